@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mrays/s (primary + shadow) and ms/frame, 1/2/4/8 GPUs.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+A step is one frame of the BASELINE config (default C3: 1920x1080, 64 spp,
+100k spheres, depth-7 octree).  N=1 renders the whole frame; N>1 deals 64x64
+tiles round-robin over the ranks, each rank renders its tiles
+into a packed slab, the slabs are gathered to rank 0 over RCCL and unpacked
+into the frame there — the gather is inside the timed step.  The frame is the
+same for every N (strong scaling, BASELINE metric "at 1920x1080").
+
+Rank 0 prints ONE JSON line.  Rays are counted by the kernel (primary + shadow
+rays actually cast) — the counts equal the CPU oracle's (tests/test_gpu_parity).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+NODE_BYTES = 8     # uint2 node record
+PRIM_BYTES = 16    # float4 sphere record per ray-sphere test
+PIXEL_BYTES = 4    # RGBA8 framebuffer write
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="target CPU-baseline sample duration")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
+                    help="PMC traffic summary written by tools/pmc_traffic.py")
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, K, pose, target_s: float) -> dict:
+    """The oracle (scalar C port, OpenMP over rows) on a bounded row sample."""
+    import numpy as np
+
+    import oracle
+    import raytracingstudy_amd as rt
+
+    sp, al = rt.generate_spheres(cfg.n_spheres, rt.SEED)
+    sc = oracle.Scene(sp, al, max_depth=cfg.max_depth)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or oracle.max_threads()
+    # calibrate on one row, then take every step-th row for ~target_s seconds
+    t = time.perf_counter()
+    _, _, c = sc.render(cfg.width, cfg.height, pose, K, spp=cfg.spp, rect=(0, cfg.height // 2, cfg.width,
+                        cfg.height // 2 + 1), n_threads=1, radiance=False)
+    one_row = max(time.perf_counter() - t, 1e-4)
+    rows = max(1, min(cfg.height, int(target_s * threads * 0.8 / one_row)))
+    step = max(1, cfg.height // rows)
+    t = time.perf_counter()
+    _, _, c = sc.render(cfg.width, cfg.height, pose, K, spp=cfg.spp, row_step=step, row_phase=step // 2,
+                        n_threads=threads, radiance=False)
+    el = time.perf_counter() - t
+    rays = int(c[0]) + int(c[1])
+    n_rows = len(range(step // 2, cfg.height, step))
+    return {"value": round(rays / el / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{cfg.name} scene, every {step}th row ({n_rows} rows x {cfg.width} px x "
+                      f"{cfg.spp} spp = {int(c[0])} primary + {int(c[1])} shadow rays) in {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import raytracingstudy_amd as rt
+    from raytracingstudy_amd.camera import scene_pose
+    from raytracingstudy_amd import tiles as T
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    cfg = rt.CONFIGS[args.config]
+    if cfg.mode != "scene":
+        raise SystemExit("bench runs a scene config (c2..c5)")
+
+    sp, al = rt.generate_spheres(cfg.n_spheres, rt.SEED)
+    r = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=cfg.spp, device=local,
+                          light_dir=rt.configs.LIGHT_DIR, ambient=rt.configs.AMBIENT)
+    r.resize(cfg.width, cfg.height)
+    pose = scene_pose()
+    r.setPosition(pose)
+    info = r.set_scene(sp, al, max_depth=cfg.max_depth, leaf_capacity=rt.configs.LEAF_CAPACITY)
+    _, K = r.camera()
+
+    dev = torch.device("cuda", local)
+    # a real (non-null) stream: the kernels, the HIP events and RCCL all run on it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    sptr = stream.cuda_stream
+    assert sptr, "need a non-null HIP stream handle
+    W, H, ts = cfg.width, cfg.height, rt.configs.TILE_SIZE
+    frame = torch.empty(W * H * 4, dtype=torch.uint8, device=dev)
+    if world > 1:
+        my_ids = T.tiles_for_rank(W, H, rank, world, ts)
+        slab = T.slab_tiles(W, H, world, ts)
+        packed = torch.zeros(slab * ts * ts * 4, dtype=torch.uint8, device=dev)
+        all_ids = [T.tiles_for_rank(W, H, k, world, ts) for k in range(world)]
+        gathered = [torch.empty_like(packed) for _ in range(world)] if rank == 0 else None
+
+    events = []
+
+    def step(record: bool):
+        if record:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        if world == 1:
+            r.render(frame.data_ptr(), sptr)
+        else:
+            r.render_tiles(my_ids, ts, packed.data_ptr(), sptr)
+        if record:
+            e1.record(stream)
+            events.append((e0, e1))
+        if world > 1:
+            dist.gather(packed, gathered, dst=0)
+            if rank == 0:
+                for k in range(world):
+                    r.unpack_tiles(gathered[k].data_ptr(), all_ids[k], ts, frame.data_ptr(), sptr)
+
+    # counted rays of one frame on this rank (deterministic; equal to the oracle's)
+    if world == 1:
+        st = r.render(frame.data_ptr(), sptr, stats=True)
+    else:
+        st = r.render_tiles(my_ids, ts, packed.data_ptr(), sptr, stats=True)
+    cnt = torch.tensor([st.primary_rays, st.shadow_rays, st.nodes_visited, st.prims_tested],
+                       dtype=torch.float64, device=dev)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else float("nan")
+    el_t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    tot = cnt.clone()
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    elapsed = float(el_t.item())
+    rays_frame = float(tot[0].item() + tot[1].item())
+
+    if rank == 0:
+        value = rays_frame * args.steps / elapsed / 1e6
+        # roofline of the dominant kernel on this rank: algorithmic bytes per launch
+        pix = (W * H) if world == 1 else len(my_ids) * ts * ts
+        alg_bytes = float(cnt[2].item()) * NODE_BYTES + float(cnt[3].item()) * PRIM_BYTES + pix * PIXEL_BYTES
+        achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+        traffic = None
+        try:
+            with open(args.pmc) as f:
+                pm = json.load(f)
+            ent = pm.get(cfg.name)
+            if ent and ent.get("n_gpus", 1) == world:
+                traffic = ent.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        out = {
+            "metric": f"Mrays/s (primary+shadow) at {W}x{H}, {cfg.spp} spp, {cfg.n_spheres} spheres",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded spheres, SURVEY.md 8d)",
+            "config": {
+                "workload": f"{cfg.name}: {cfg.note}",
+                "width": W, "height": H, "spp": cfg.spp, "n_spheres": cfg.n_spheres,
+                "octree_depth": info["max_depth"], "octree_nodes": info["n_nodes"],
+                "prim_refs": info["n_prim_refs"], "leaf_capacity": rt.configs.LEAF_CAPACITY,
+                "parallelism": f"tiles{ts}x{world}" if world > 1 else "single",
+                "rays_per_frame": int(rays_frame),
+                "primary_per_frame": int(tot[0].item()), "shadow_per_frame": int(tot[1].item()),
+                "kernel_ms": round(kern_ms, 4),
+                "scene_build_ms": round(info["build_ms"], 1),
+                "scene_upload_ms": round(info["upload_ms"], 1),
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "alg_bytes_per_launch": int(alg_bytes),
+                "per_ray": {"nodes": float(cnt[2].item()) / float(cnt[0].item() + cnt[1].item()),
+                            "prims": float(cnt[3].item()) / float(cnt[0].item() + cnt[1].item())},
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and args.cpu_baseline == "auto":
+            try:
+                out["cpu_baseline"] = cpu_baseline(cfg, K, pose, args.cpu_seconds)
+            except Exception as e:  # reported, never fatal for the GPU number
+                out["cpu_baseline"] = {"error": repr(e)}
+        print(json.dumps(out), flush=True)
+    r.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

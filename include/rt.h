@@ -1,0 +1,198 @@
+/*
+ * rt.h — C-ABI of the MI355X-native render path (drop-in for the reference's
+ * KernelRenderer, randomwons/RayTracingStudy).
+ *
+ * Plain C: opaque handle, plain pointers and sizes, int status (0 = ok,
+ * negative = error).  No HIP, GL or torch types appear in any signature; a HIP
+ * stream is passed as `void*` (a hipStream_t), device buffers as `void*`.
+ *
+ * Every entry point names the reference interface it replaces (file:line is
+ * relative to the reference repository root):
+ *
+ *   reference                                            this ABI
+ *   ---------------------------------------------------  ---------------------------
+ *   KernelRenderer(cudaGraphicsResource_t,w,h)            rt_create
+ *     include/renderer.cuh:29, src/renderer.cu:124-141
+ *   ~KernelRenderer()  include/renderer.cuh:28,           rt_destroy
+ *     src/renderer.cu:189-198 (leaks device objects)
+ *   setPosition(glm::mat4)  include/renderer.cuh:32,      rt_set_pose
+ *     src/renderer.cu:111-113, 93-97
+ *   setIntrinsic(glm::mat3) include/renderer.cuh:33,      rt_set_intrinsic
+ *     src/renderer.cu:115-117, 99-103
+ *   resize(int,int) include/renderer.cuh:31,              rt_resize
+ *     src/renderer.cu:155-187
+ *   setOctree(vec3,vec3,float) include/renderer.cuh:35    rt_set_octree
+ *     (declared, never defined: src/renderer.cu:119-121)
+ *   (none: Octree::traverse is a stub,                    rt_set_scene
+ *     include/octree.h:19-21)
+ *   render() include/renderer.cuh:30,                     rt_render
+ *     src/renderer.cu:143-153 (raytracing<<<>>> :149)
+ *   cudaGraphicsResourceGetMappedPointer + unmap          rt_render(dev_rgba8 = mapped ptr)
+ *     src/renderer.cu:145-151
+ *   (none: single device)                                 rt_render_tiles / rt_unpack_tiles
+ *   (none: no error reporting, all void)                  rt_last_error
+ *
+ * Threading: one handle per host thread / stream; calls on one handle are not
+ * re-entrant.  Ownership: the caller owns every buffer it passes in; the
+ * renderer owns its internal device buffers (freed by rt_destroy).
+ */
+#ifndef RT_AMD_RT_H
+#define RT_AMD_RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+typedef struct rt_renderer rt_renderer;
+
+/* status codes */
+enum {
+    RT_OK = 0,
+    RT_E_INVALID = -1,  /* bad argument */
+    RT_E_HIP = -2,      /* HIP runtime error (message in rt_last_error) */
+    RT_E_NOMEM = -3,    /* host or device allocation failed */
+    RT_E_NOSCENE = -4,  /* RT_MODE_SCENE render without rt_set_scene */
+    RT_E_STATE = -5     /* call not valid in the current state */
+};
+
+/* render modes */
+enum {
+    /* Byte-exact restatement of the reference kernel `raytracing`
+     * (src/renderer.cu:57-82): R = Octree::traverse() = 200, root-box slab test
+     * `hit_sphere` (src/renderer.cu:3-55), miss colour from the direction. */
+    RT_MODE_COMPAT = 0,
+    /* Build-defined octree scene: nearest sphere hit, Lambert + one shadow ray,
+     * `spp` jittered samples averaged (DESIGN.md "Scene mode"). */
+    RT_MODE_SCENE = 1
+};
+
+/* rt_config.flags */
+enum {
+    RT_FLAG_JITTER = 1u << 0,      /* per-sample sub-pixel jitter (default: on iff spp > 1) */
+    RT_FLAG_NO_JITTER = 1u << 1,   /* force jitter off */
+    RT_FLAG_RADIANCE = 1u << 2,    /* also keep the float4 mean radiance buffer */
+    RT_FLAG_NO_SHADOWS = 1u << 3   /* skip shadow rays (Lambert without visibility) */
+};
+
+typedef struct rt_config {
+    uint32_t width;        /* framebuffer width  (reference: KernelRenderer::width)  */
+    uint32_t height;       /* framebuffer height (reference: KernelRenderer::height) */
+    uint32_t spp;          /* samples per pixel (scene mode; compat ignores it: 1)   */
+    uint32_t seed;         /* sampling seed (scene mode)                              */
+    int32_t device;        /* HIP device ordinal, -1 = the calling thread's current   */
+    uint32_t mode;         /* RT_MODE_*                                               */
+    uint32_t flags;        /* RT_FLAG_*                                               */
+    float light_dir[3];    /* direction the directional light TRAVELS (need not be unit) */
+    float ambient;         /* ambient term of the Lambert shade, [0,1]                */
+} rt_config;
+
+/* Octree parameters.  Defaults (rt_octree_params_default) are the reference's
+ * hard-coded root, src/renderer.cu:134-136: min (0,0,0), max (1.28)^3,
+ * resolution 0.01 => max_depth = ceil(log2(1.28/0.01)) = 7. */
+typedef struct rt_octree_params {
+    float min[3];
+    float max[3];
+    float resolution;       /* smallest cell edge; used when max_depth == 0            */
+    uint32_t max_depth;     /* 0 = derive from resolution; else 1..16                  */
+    uint32_t leaf_capacity; /* split a cell while it holds more spheres than this (8) */
+} rt_octree_params;
+
+typedef struct rt_stats {
+    uint64_t primary_rays;   /* camera rays cast (pixels * spp)                         */
+    uint64_t shadow_rays;    /* shadow rays cast (lit-facing primary hits)              */
+    uint64_t nodes_visited;  /* octree node records read (DESIGN.md counter definition) */
+    uint64_t prims_tested;   /* ray-sphere tests                                        */
+    float ms;                /* device time of the render launch(es), hipEvent          */
+    uint32_t reserved;
+} rt_stats;
+
+typedef struct rt_scene_info {
+    uint32_t n_spheres;
+    uint32_t n_nodes;        /* node records (internal + leaf)                          */
+    uint32_t n_leaves;
+    uint32_t n_prim_refs;    /* total length of all leaf sphere lists                   */
+    uint32_t max_depth;      /* depth limit the tree was built with                     */
+    uint32_t depth_reached;  /* deepest leaf                                            */
+    uint32_t node_bytes;     /* sizeof one node record                                  */
+    uint32_t prim_bytes;     /* bytes read per sphere test                              */
+    double build_ms;         /* host build time                                         */
+    double upload_ms;        /* host->device upload time                                */
+} rt_scene_info;
+
+/* ---- version / discovery -------------------------------------------------- */
+int rt_abi_version(void);
+/* Number of visible HIP devices (0 when no GPU); never initialises a context. */
+int rt_device_count(void);
+
+/* ---- lifecycle ------------------------------------------------------------ */
+void rt_config_default(rt_config* cfg);
+void rt_octree_params_default(rt_octree_params* p);
+/* Reference ctor: camera K0 = mat3(1000,0,640, 0,1000,340, 0,0,1) and identity
+ * pose (src/renderer.cu:84-91), octree root from rt_octree_params_default. */
+int rt_create(const rt_config* cfg, rt_renderer** out);
+int rt_destroy(rt_renderer* r);
+
+/* ---- camera --------------------------------------------------------------- */
+/* pose: glm-style column-major mat4; origin = pose[3].xyz, rot = mat3(pose)
+ * (include/camera.h:43-46).  K: column-major mat3, K[0][0]=fx, K[1][1]=fy,
+ * K[0][2]=cx, K[1][2]=cy, i.e. K[c*3+r] (include/camera.h:24-26). */
+int rt_set_pose(rt_renderer* r, const float pose[16]);
+int rt_set_intrinsic(rt_renderer* r, const float K[9]);
+int rt_get_camera(const rt_renderer* r, float pose_out[16], float K_out[9]);
+/* Reference resize (src/renderer.cu:155-170): f = W/(2 tan(radians(80)/2)),
+ * cx = W/2, cy = H/2 (integer division); reallocates internal buffers. */
+int rt_resize(rt_renderer* r, uint32_t width, uint32_t height);
+/* The intrinsic rt_resize would set, without a renderer (for hosts/tests). */
+void rt_resize_intrinsic(uint32_t width, uint32_t height, float K_out[9]);
+
+/* ---- scene ---------------------------------------------------------------- */
+/* spheres: 4*n floats (cx, cy, cz, radius); albedo: n packed RGBA8 (R in the low
+ * byte) or NULL (every sphere 0.8 grey).  oct == NULL keeps the current octree
+ * parameters.  Builds the octree on the host and uploads it. */
+int rt_set_scene(rt_renderer* r, const float* spheres, const uint32_t* albedo, uint32_t n,
+                 const rt_octree_params* oct);
+/* Mirror of the reference's setOctree(min, max, resolution): rebuilds the
+ * octree of the current spheres with a new root box / resolution. */
+int rt_set_octree(rt_renderer* r, const float min[3], const float max[3], float resolution);
+int rt_get_scene_info(const rt_renderer* r, rt_scene_info* info);
+/* Synthetic scene generator: splitmix64 -> PCG32 from `seed`;
+ * centres U[0,1.28)^3, radius 0.02*(1000/n)^(1/3)*U[0.5,1), albedo U[0.2,1). */
+int rt_generate_spheres(uint32_t n, uint32_t seed, float* spheres_out, uint32_t* albedo_out);
+
+/* ---- render --------------------------------------------------------------- */
+/* Render one frame.  dev_rgba8: W*H*4 device bytes (e.g. the pointer a GL PBO
+ * maps to), or NULL to render into the renderer's internal framebuffer.
+ * stream: a hipStream_t or NULL (the renderer's own stream).  Asynchronous
+ * unless stats != NULL (then it waits for the frame and fills the counters). */
+int rt_render(rt_renderer* r, void* dev_rgba8, void* stream, rt_stats* stats);
+/* Render only the listed image tiles (tile_size x tile_size, row-major tile
+ * ids over ceil(W/ts) x ceil(H/ts)) into a packed device buffer of
+ * n_tiles*ts*ts*4 bytes: tile k's pixel (lx,ly) at byte 4*(k*ts*ts + ly*ts + lx);
+ * pixels outside the image are written as 0.  Used to shard a frame over GPUs. */
+int rt_render_tiles(rt_renderer* r, const uint32_t* tile_ids, uint32_t n_tiles,
+                    uint32_t tile_size, void* dev_packed_rgba8, void* stream, rt_stats* stats);
+/* Scatter a packed tile buffer (layout above) into a W*H*4 device image. */
+int rt_unpack_tiles(rt_renderer* r, const void* dev_packed_rgba8, const uint32_t* tile_ids,
+                    uint32_t n_tiles, uint32_t tile_size, void* dev_rgba8, void* stream);
+/* Wait for all work queued by this renderer. */
+int rt_synchronize(rt_renderer* r);
+/* Copy the internal framebuffer (and the float4 radiance buffer when
+ * RT_FLAG_RADIANCE is set) to host memory; either pointer may be NULL. */
+int rt_readback(rt_renderer* r, uint8_t* host_rgba8, float* host_rgba32f);
+/* Device pointer of the internal framebuffer (W*H*4 bytes). */
+void* rt_framebuffer(rt_renderer* r);
+
+/* ---- errors --------------------------------------------------------------- */
+/* Last error message for this handle (r may be NULL: last global error). */
+const char* rt_last_error(const rt_renderer* r);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_AMD_RT_H */

@@ -1,0 +1,651 @@
+/*
+ * oracle.c — TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *
+ * Plain-C CPU restatement of:
+ *   - the reference kernel `raytracing` (src/renderer.cu:57-82) with
+ *     Camera::getRay (include/camera.h:24-41), hit_sphere
+ *     (src/renderer.cu:3-55) and the resize intrinsic (src/renderer.cu:155-170);
+ *   - the build-defined scene mode (DESIGN.md "Scene mode"): sphere generator,
+ *     octree builder, grid-space octree walk, Lambert + shadow ray, spp mean.
+ *
+ * Compiled with -O2 -ffp-contract=off (no FMA contraction, SSE f32/f64, no
+ * excess precision): every expression below is evaluated exactly in source
+ * order, which is the semantics the HIP kernels reproduce bit for bit.
+ * Never compile with -ffast-math.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ========================================================================== */
+/* compat mode                                                                */
+/* ========================================================================== */
+
+/* src/renderer.cu:162-170: intrinsic = mat3(1); f = width/(2*tan(radians(80.f)/2))
+ * (glm::radians multiplies by the float constant, glm::tan = tanf, the
+ * arithmetic is float; the double f is then stored back into a float);
+ * intrinsic[0][2] = width/2, intrinsic[1][2] = height/2 in integer arithmetic. */
+void orc_resize_intrinsic(uint32_t width, uint32_t height, float K[9]) {
+    const float rad = 80.f * 0.01745329251994329576923690768489f;
+    const float f = (float)width / (2.0f * tanf(rad / 2.0f));
+    for (int i = 0; i < 9; ++i) K[i] = 0.0f;
+    K[0] = f;                      /* [0][0] */
+    K[4] = f;                      /* [1][1] */
+    K[8] = 1.0f;                   /* [2][2] */
+    K[2] = (float)(width / 2u);    /* [0][2] */
+    K[5] = (float)(height / 2u);   /* [1][2] */
+}
+
+/* include/camera.h:24-41 (u, v already floats; the reference converts its
+ * uint32 pixel index to float in `u - intrinsic[0][2]`).  glm storage is
+ * column-major: rot[c][r] = pose[c*4+r], K[c][r] = K[c*3+r]. */
+void orc_get_ray(const float pose[16], const float K[9], float u, float v, float dir_out[3]) {
+    const float dx = (u - K[2]) / K[0];
+    const float dy = (v - K[5]) / K[4];
+    const float dz = 1.0f;
+    float wdx = pose[0] * dx + pose[4] * dy + pose[8] * dz;
+    float wdy = pose[1] * dx + pose[5] * dy + pose[9] * dz;
+    float wdz = pose[2] * dx + pose[6] * dy + pose[10] * dz;
+    const float len = sqrtf(wdx * wdx + wdy * wdy + wdz * wdz);
+    wdx /= len;
+    wdy /= len;
+    wdz /= len;
+    dir_out[0] = wdx;
+    dir_out[1] = wdy;
+    dir_out[2] = wdz;
+}
+
+/* src/renderer.cu:3-55.  Box min (0,0,0), max glm::vec3(1.28) (doubles -> f32),
+ * centre glm::vec3(0.64) passed from :70.  Mixed f32/f64 exactly as written:
+ * the mirrored origin is a float expression widened to double, the inverse is
+ * a float division widened to double, the slab products are double and
+ * rounded to float; fmaxf/fminf drop NaN (0*inf). No t >= 0 test. */
+int orc_hit_root_box(const float origin[3], const float dir[3]) {
+    const float bmin = 0.0f;
+    const float bmax = (float)1.28;
+    const float center = (float)0.64;
+    double ro[3], inv[3];
+    for (int i = 0; i < 3; ++i) {
+        if (dir[i] < 0.0f) {
+            ro[i] = (double)(center * 2.0f - origin[i]);
+            inv[i] = (double)(-(1.0f / dir[i]));
+        } else {
+            ro[i] = (double)origin[i];
+            inv[i] = (double)(1.0f / dir[i]);
+        }
+    }
+    const float tx0 = (float)(((double)bmin - ro[0]) * inv[0]);
+    const float tx1 = (float)(((double)bmax - ro[0]) * inv[0]);
+    const float ty0 = (float)(((double)bmin - ro[1]) * inv[1]);
+    const float ty1 = (float)(((double)bmax - ro[1]) * inv[1]);
+    const float tz0 = (float)(((double)bmin - ro[2]) * inv[2]);
+    const float tz1 = (float)(((double)bmax - ro[2]) * inv[2]);
+    return fmaxf(fmaxf(tx0, ty0), tz0) < fminf(fminf(tx1, ty1), tz1);
+}
+
+/* __saturatef: clamp to [0,1], NaN -> 0 */
+static inline float sat(float x) { return x > 0.0f ? (x < 1.0f ? x : 1.0f) : 0.0f; }
+
+/* src/renderer.cu:57-82.  Row-major uchar4, pid = y*W + x. */
+void orc_render_compat(uint32_t width, uint32_t height, const float pose[16], const float K[9],
+                       uint8_t* out) {
+    const float origin[3] = {pose[12], pose[13], pose[14]};
+    for (uint32_t y = 0; y < height; ++y) {
+        for (uint32_t x = 0; x < width; ++x) {
+            uint8_t* px = out + 4u * ((size_t)y * width + x);
+            float dir[3];
+            orc_get_ray(pose, K, (float)x, (float)y, dir);
+            if (orc_hit_root_box(origin, dir)) {
+                px[0] = px[1] = px[2] = px[3] = 255;
+                continue;
+            }
+            px[0] = (uint8_t)200.0; /* (unsigned char)Octree::traverse() */
+            px[1] = (uint8_t)(sat(dir[1]) * 255.0f);
+            px[2] = (uint8_t)(sat(dir[2]) * 255.0f);
+            px[3] = 255;
+        }
+    }
+}
+
+/* ========================================================================== */
+/* synthetic scene                                          */
+/* ========================================================================== */
+
+static uint64_t splitmix64(uint64_t* x) {
+    uint64_t z = (*x += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+typedef struct { uint64_t state, inc; } pcg32_t;
+
+static uint32_t pcg32_next(pcg32_t* g) {
+    const uint64_t old = g->state;
+    g->state = old * 6364136223846793005ull + g->inc;
+    const uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+    const uint32_t rot = (uint32_t)(old >> 59u);
+    return (xs >> rot) | (xs << ((-rot) & 31u));
+}
+
+static float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+
+void orc_generate_spheres(uint32_t n, uint32_t seed, float* sp, uint32_t* albedo) {
+    uint64_t sm = (uint64_t)seed;
+    pcg32_t g;
+    g.state = splitmix64(&sm);
+    g.inc = splitmix64(&sm) | 1ull;
+    const float rscale = n ? (float)(0.02 * cbrt(1000.0 / (double)n)) : 0.0f;
+    for (uint32_t i = 0; i < n; ++i) {
+        const float cx = u01(pcg32_next(&g)) * 1.28f;
+        const float cy = u01(pcg32_next(&g)) * 1.28f;
+        const float cz = u01(pcg32_next(&g)) * 1.28f;
+        const float ru = u01(pcg32_next(&g));
+        sp[4 * i + 0] = cx;
+        sp[4 * i + 1] = cy;
+        sp[4 * i + 2] = cz;
+        sp[4 * i + 3] = rscale * (0.5f + 0.5f * ru);
+        uint32_t a = 0xFF000000u;
+        for (int c = 0; c < 3; ++c) {
+            const float v = 0.2f + 0.8f * u01(pcg32_next(&g));
+            a |= ((uint32_t)(v * 255.0f) & 0xFFu) << (8 * c);
+        }
+        if (albedo) albedo[i] = a;
+    }
+}
+
+static inline uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+uint32_t orc_sample_hash(uint32_t seed, uint32_t pid, uint32_t s, uint32_t dim) {
+    return mix32(mix32(mix32(seed ^ 0x9E3779B9u) ^ pid) ^ ((s << 1) | dim));
+}
+
+/* ========================================================================== */
+/* octree                                                                     */
+/* ========================================================================== */
+
+typedef struct {
+    int32_t child[8]; /* real child index (bit0 x, bit1 y, bit2 z) -> node, -1 empty */
+    int32_t leaf;
+    uint32_t off, cnt; /* leaf: range in prim list */
+} onode;
+
+struct orc_scene {
+    const float* spheres; /* borrowed copy (owned below) */
+    float* sp;
+    uint32_t* albedo;
+    uint32_t n;
+    float rmin[3], rmax[3];
+    uint32_t max_depth, leaf_cap;
+    onode* nodes;
+    uint32_t n_nodes, cap_nodes;
+    uint32_t* prims;
+    uint32_t n_prims, cap_prims;
+    uint32_t n_leaves, depth_reached;
+    /* traversal constants */
+    float scale[3];
+    float G;
+};
+
+static uint32_t new_node(orc_scene* s) {
+    if (s->n_nodes == s->cap_nodes) {
+        s->cap_nodes = s->cap_nodes ? 2 * s->cap_nodes : 1024;
+        s->nodes = (onode*)realloc(s->nodes, sizeof(onode) * s->cap_nodes);
+    }
+    onode* nd = &s->nodes[s->n_nodes];
+    for (int i = 0; i < 8; ++i) nd->child[i] = -1;
+    nd->leaf = 0;
+    nd->off = nd->cnt = 0;
+    return s->n_nodes++;
+}
+
+static void push_prim(orc_scene* s, uint32_t idx) {
+    if (s->n_prims == s->cap_prims) {
+        s->cap_prims = s->cap_prims ? 2 * s->cap_prims : 4096;
+        s->prims = (uint32_t*)realloc(s->prims, sizeof(uint32_t) * s->cap_prims);
+    }
+    s->prims[s->n_prims++] = idx;
+}
+
+/* Conservative sphere/cell overlap in double: squared distance from the centre
+ * to the closed cell box <= (r + margin)^2, margin = 1e-6 * largest extent. */
+static int overlaps(const float* sp, const double lo[3], const double hi[3], double margin) {
+    double d2 = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        const double c = (double)sp[i];
+        if (c < lo[i]) {
+            const double e = lo[i] - c;
+            d2 += e * e;
+        } else if (c > hi[i]) {
+            const double e = c - hi[i];
+            d2 += e * e;
+        }
+    }
+    const double r = (double)sp[3] + margin;
+    return d2 <= r * r;
+}
+
+static void cell_bounds(const orc_scene* s, uint32_t depth, const uint32_t c[3], double lo[3],
+                        double hi[3]) {
+    const double cells = (double)(1u << depth);
+    for (int i = 0; i < 3; ++i) {
+        const double ext = (double)s->rmax[i] - (double)s->rmin[i];
+        lo[i] = (double)s->rmin[i] + ext * ((double)c[i] / cells);
+        hi[i] = (double)s->rmin[i] + ext * ((double)(c[i] + 1u) / cells);
+    }
+}
+
+static double margin_of(const orc_scene* s) {
+    double m = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        const double e = (double)s->rmax[i] - (double)s->rmin[i];
+        if (e > m) m = e;
+    }
+    return 1e-6 * m;
+}
+
+/* Recursive build: split while count > leaf_cap and depth < max_depth; a
+ * child is kept only when some sphere overlaps it; leaf lists ascending. */
+static void build_rec(orc_scene* s, uint32_t node, uint32_t depth, const uint32_t c[3],
+                      const uint32_t* list, uint32_t cnt) {
+    if (cnt <= s->leaf_cap || depth >= s->max_depth) {
+        s->nodes[node].leaf = 1;
+        s->nodes[node].off = s->n_prims;
+        s->nodes[node].cnt = cnt;
+        for (uint32_t i = 0; i < cnt; ++i) push_prim(s, list[i]);
+        s->n_leaves++;
+        if (depth > s->depth_reached) s->depth_reached = depth;
+        return;
+    }
+    const double margin = margin_of(s);
+    uint32_t* sub = (uint32_t*)malloc(sizeof(uint32_t) * (cnt ? cnt : 1));
+    for (uint32_t ch = 0; ch < 8; ++ch) {
+        const uint32_t cc[3] = {2 * c[0] + (ch & 1u), 2 * c[1] + ((ch >> 1) & 1u),
+                                2 * c[2] + ((ch >> 2) & 1u)};
+        double lo[3], hi[3];
+        cell_bounds(s, depth + 1, cc, lo, hi);
+        uint32_t m = 0;
+        for (uint32_t i = 0; i < cnt; ++i)
+            if (overlaps(s->sp + 4u * list[i], lo, hi, margin)) sub[m++] = list[i];
+        if (!m) continue;
+        const uint32_t k = new_node(s);
+        s->nodes[node].child[ch] = (int32_t)k;
+        build_rec(s, k, depth + 1, cc, sub, m);
+    }
+    free(sub);
+}
+
+uint32_t orc_depth_for_resolution(const float rmin[3], const float rmax[3], float res) {
+    float ext = 0.0f;
+    for (int i = 0; i < 3; ++i)
+        if (rmax[i] - rmin[i] > ext) ext = rmax[i] - rmin[i];
+    if (!(res > 0.0f)) return 7;
+    uint32_t d = 0;
+    while (d < 16 && (double)ext / (double)(1u << d) > (double)res * (1.0 + 1e-6)) ++d;
+    return d;
+}
+
+orc_scene* orc_scene_build(const float* spheres, const uint32_t* albedo, uint32_t n,
+                           const float root_min[3], const float root_max[3], uint32_t max_depth,
+                           uint32_t leaf_capacity) {
+    orc_scene* s = (orc_scene*)calloc(1, sizeof(orc_scene));
+    s->n = n;
+    s->sp = (float*)malloc(sizeof(float) * 4u * (n ? n : 1));
+    memcpy(s->sp, spheres, sizeof(float) * 4u * n);
+    s->spheres = s->sp;
+    s->albedo = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+    for (uint32_t i = 0; i < n; ++i) s->albedo[i] = albedo ? albedo[i] : 0xFFCCCCCCu;
+    for (int i = 0; i < 3; ++i) {
+        s->rmin[i] = root_min[i];
+        s->rmax[i] = root_max[i];
+    }
+    s->max_depth = max_depth > 16 ? 16 : max_depth;
+    s->leaf_cap = leaf_capacity;
+    s->G = (float)(1u << s->max_depth);
+    for (int i = 0; i < 3; ++i) s->scale[i] = s->G / (root_max[i] - root_min[i]);
+
+    const double margin = margin_of(s);
+    const uint32_t zero[3] = {0, 0, 0};
+    double lo[3], hi[3];
+    cell_bounds(s, 0, zero, lo, hi);
+    uint32_t* list = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        if (overlaps(s->sp + 4u * i, lo, hi, margin)) list[m++] = i;
+    const uint32_t root = new_node(s);
+    build_rec(s, root, 0, zero, list, m);
+    free(list);
+    return s;
+}
+
+void orc_scene_free(orc_scene* s) {
+    if (!s) return;
+    free(s->sp);
+    free(s->albedo);
+    free(s->nodes);
+    free(s->prims);
+    free(s);
+}
+
+void orc_scene_info(const orc_scene* s, uint32_t info[4]) {
+    info[0] = s->n_nodes;
+    info[1] = s->n_leaves;
+    info[2] = s->n_prims;
+    info[3] = s->depth_reached;
+}
+
+/* ---- ray / sphere ---------------------------------------------------------- */
+
+/* Nearest root of |o + t d - c| = r with the perpendicular-distance
+ * discriminant (no b*b - c cancellation); accepted iff tmin < t < tmax. */
+static inline int isect(const float o[3], const float d[3], const float* sp, float tmin,
+                        float tmax, float* tout) {
+    const float ocx = o[0] - sp[0];
+    const float ocy = o[1] - sp[1];
+    const float ocz = o[2] - sp[2];
+    const float b = ocx * d[0] + ocy * d[1] + ocz * d[2];
+    const float qx = ocx - b * d[0];
+    const float qy = ocy - b * d[1];
+    const float qz = ocz - b * d[2];
+    const float r = sp[3];
+    const float h = r * r - (qx * qx + qy * qy + qz * qz);
+    if (h < 0.0f) return 0;
+    const float sq = sqrtf(h);
+    float t = -b - sq;
+    if (!(t > tmin)) t = -b + sq;
+    if (!(t > tmin) || !(t < tmax)) return 0;
+    *tout = t;
+    return 1;
+}
+
+/* ---- octree walk (DESIGN.md "Octree walk") --------------------------------- */
+
+typedef struct {
+    float og[3];   /* origin in (mirrored) grid units */
+    float inv[3];  /* 1 / (|d| * scale), |d| clamped to >= 1e-20 */
+    uint32_t mask; /* bit i: axis i mirrored (d_i < 0) */
+} walk_t;
+
+static inline float plane(const walk_t* w, int i, uint32_t k) {
+    return ((float)k - w->og[i]) * w->inv[i];
+}
+
+static int walk(const orc_scene* s, const float o[3], const float d[3], float tmin, float tmax,
+                int any_hit, float* t_out, uint32_t* idx_out, uint64_t* nodes, uint64_t* prims) {
+    walk_t w;
+    w.mask = 0;
+    const uint32_t G = 1u << s->max_depth;
+    for (int i = 0; i < 3; ++i) {
+        const float g = (o[i] - s->rmin[i]) * s->scale[i];
+        const int neg = d[i] < 0.0f;
+        float a = fabsf(d[i]);
+        if (a < 1e-20f) a = 1e-20f;
+        w.og[i] = neg ? s->G - g : g;
+        w.inv[i] = 1.0f / (a * s->scale[i]);
+        w.mask |= (uint32_t)neg << i;
+    }
+    float t0 = plane(&w, 0, 0), t1 = plane(&w, 0, G);
+    for (int i = 1; i < 3; ++i) {
+        const float a0 = plane(&w, i, 0), a1 = plane(&w, i, G);
+        if (a0 > t0) t0 = a0;
+        if (a1 < t1) t1 = a1;
+    }
+    if (t0 < tmin) t0 = tmin;
+    if (t1 > tmax) t1 = tmax;
+    if (!(t0 < t1)) return 0;
+
+    float best_t = tmax;
+    uint32_t best = 0xFFFFFFFFu;
+    const onode* N = s->nodes;
+    *nodes += 1; /* root record */
+    if (N[0].leaf) {
+        for (uint32_t j = 0; j < N[0].cnt; ++j) {
+            const uint32_t idx = s->prims[N[0].off + j];
+            float t;
+            *prims += 1;
+            if (isect(o, d, s->sp + 4u * idx, tmin, tmax, &t)) {
+                if (any_hit) {
+                    *t_out = t;
+                    *idx_out = idx;
+                    return 1;
+                }
+                if (t < best_t || (t == best_t && idx < best)) {
+                    best_t = t;
+                    best = idx;
+                }
+            }
+        }
+    } else {
+        uint32_t stack[17];
+        uint32_t depth = 0, c[3] = {0, 0, 0};
+        uint32_t node = 0;
+        stack[0] = 0;
+        float t = t0;
+        for (uint32_t it = 0, cap = 8u * G + 64u; it < cap; ++it) { /* same cap as the kernel */
+            const uint32_t half = G >> (depth + 1);
+            uint32_t bits = 0;
+            for (int i = 0; i < 3; ++i)
+                if (plane(&w, i, (2u * c[i] + 1u) * half) <= t) bits |= 1u << i;
+            const uint32_t child = bits ^ w.mask;
+            for (int i = 0; i < 3; ++i) c[i] = 2u * c[i] + ((bits >> i) & 1u);
+            depth += 1;
+            const int32_t ch = N[node].child[child];
+            if (ch >= 0) {
+                *nodes += 1;
+                if (!N[ch].leaf) {
+                    node = (uint32_t)ch;
+                    stack[depth] = node;
+                    continue;
+                }
+                for (uint32_t j = 0; j < N[ch].cnt; ++j) {
+                    const uint32_t idx = s->prims[N[ch].off + j];
+                    float th;
+                    *prims += 1;
+                    if (isect(o, d, s->sp + 4u * idx, tmin, tmax, &th)) {
+                        if (any_hit) {
+                            *t_out = th;
+                            *idx_out = idx;
+                            return 1;
+                        }
+                        if (th < best_t || (th == best_t && idx < best)) {
+                            best_t = th;
+                            best = idx;
+                        }
+                    }
+                }
+            }
+            /* leave the leaf / empty cell at `depth`, coords c */
+            const uint32_t size = G >> depth;
+            float e[3];
+            for (int i = 0; i < 3; ++i) e[i] = plane(&w, i, (c[i] + 1u) * size);
+            float texit = e[0] < e[1] ? e[0] : e[1];
+            texit = texit < e[2] ? texit : e[2];
+            if (best_t < texit) break;
+            if (texit >= t1) break;
+            uint32_t diff = 0, out = 0;
+            for (int i = 0; i < 3; ++i) {
+                if (e[i] == texit) {
+                    diff |= c[i] ^ (c[i] + 1u);
+                    c[i] += 1u;
+                    if (c[i] >= (1u << depth)) out = 1;
+                }
+            }
+            if (out) break;
+            const uint32_t m = 32u - (uint32_t)__builtin_clz(diff);
+            depth -= m;
+            for (int i = 0; i < 3; ++i) c[i] >>= m;
+            node = stack[depth];
+            t = texit;
+        }
+    }
+    if (best != 0xFFFFFFFFu) {
+        *t_out = best_t;
+        *idx_out = best;
+        return 1;
+    }
+    return 0;
+}
+
+int orc_trace(const orc_scene* s, const float o[3], const float d[3], float tmin, float tmax,
+              int any_hit, float* t_out, uint32_t* idx_out, uint64_t counters[4]) {
+    uint64_t nodes = 0, prims = 0;
+    const int h = walk(s, o, d, tmin, tmax, any_hit, t_out, idx_out, &nodes, &prims);
+    if (counters) {
+        counters[2] += nodes;
+        counters[3] += prims;
+    }
+    return h;
+}
+
+/* Brute force over every sphere (cross-check of the walk's conservativeness). */
+int orc_trace_brute(const orc_scene* s, const float o[3], const float d[3], float tmin,
+                    float tmax, int any_hit, float* t_out, uint32_t* idx_out) {
+    float best_t = tmax;
+    uint32_t best = 0xFFFFFFFFu;
+    for (uint32_t i = 0; i < s->n; ++i) {
+        float t;
+        if (isect(o, d, s->sp + 4u * i, tmin, tmax, &t)) {
+            if (any_hit) {
+                *t_out = t;
+                *idx_out = i;
+                return 1;
+            }
+            if (t < best_t || (t == best_t && i < best)) {
+                best_t = t;
+                best = i;
+            }
+        }
+    }
+    if (best == 0xFFFFFFFFu) return 0;
+    *t_out = best_t;
+    *idx_out = best;
+    return 1;
+}
+
+/* ========================================================================== */
+/* scene render (DESIGN.md "Scene mode")                                      */
+/* ========================================================================== */
+
+#define SHADOW_EPS 1e-5f
+
+void orc_render_scene(const orc_scene* s, uint32_t W, uint32_t H, const float pose[16],
+                      const float K[9], uint32_t spp, uint32_t seed, uint32_t flags,
+                      const float light_dir[3], float ambient, uint32_t x0, uint32_t y0,
+                      uint32_t x1, uint32_t y1, uint32_t row_step, uint32_t row_phase,
+                      uint8_t* out8, float* out32, uint64_t counters[4], int n_threads) {
+    const float origin[3] = {pose[12], pose[13], pose[14]};
+    const int jitter = (flags & 1u) != 0;
+    const int shadows = (flags & 8u) == 0;
+    /* L = -normalize(light_dir): direction toward the light */
+    const float ll = sqrtf(light_dir[0] * light_dir[0] + light_dir[1] * light_dir[1] +
+                           light_dir[2] * light_dir[2]);
+    const float L[3] = {-(light_dir[0] / ll), -(light_dir[1] / ll), -(light_dir[2] / ll)};
+    const float inv_spp = 1.0f / (float)spp;
+    const float miss_r = 200.0f / 255.0f;
+    const uint32_t seedmix = mix32(seed ^ 0x9E3779B9u);
+    if (x1 > W) x1 = W;
+    if (y1 > H) y1 = H;
+    if (row_step == 0) row_step = 1;
+    uint64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#else
+    (void)n_threads;
+#endif
+    const long ny = (long)y1 - (long)y0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : c0, c1, c2, c3)
+    for (long yy = 0; yy < (ny > 0 ? ny : 0); ++yy) {
+        const uint32_t y = y0 + (uint32_t)yy;
+        if (y % row_step != row_phase % row_step) continue;
+        for (uint32_t x = x0; x < x1; ++x) {
+            const uint32_t pid = y * W + x;
+            const uint32_t hp = mix32(seedmix ^ pid);
+            float ar = 0.0f, ag = 0.0f, ab = 0.0f;
+            for (uint32_t sidx = 0; sidx < spp; ++sidx) {
+                float u = (float)x, v = (float)y;
+                if (jitter) {
+                    u = u + u01(mix32(hp ^ (sidx << 1)));
+                    v = v + u01(mix32(hp ^ ((sidx << 1) | 1u)));
+                }
+                float d[3];
+                orc_get_ray(pose, K, u, v, d);
+                c0 += 1;
+                float t;
+                uint32_t idx;
+                uint64_t nn = 0, pp = 0;
+                float cr, cg, cb;
+                if (!walk(s, origin, d, 0.0f, INFINITY, 0, &t, &idx, &nn, &pp)) {
+                    cr = miss_r;
+                    cg = sat(d[1]);
+                    cb = sat(d[2]);
+                } else {
+                    const float* sp = s->sp + 4u * idx;
+                    const float p[3] = {origin[0] + t * d[0], origin[1] + t * d[1],
+                                        origin[2] + t * d[2]};
+                    const float ir = 1.0f / sp[3];
+                    const float n[3] = {(p[0] - sp[0]) * ir, (p[1] - sp[1]) * ir,
+                                        (p[2] - sp[2]) * ir};
+                    const float ndl = n[0] * L[0] + n[1] * L[1] + n[2] * L[2];
+                    float lam = ndl > 0.0f ? ndl : 0.0f;
+                    if (ndl > 0.0f && shadows) {
+                        const float so[3] = {p[0] + n[0] * SHADOW_EPS, p[1] + n[1] * SHADOW_EPS,
+                                             p[2] + n[2] * SHADOW_EPS};
+                        float ts;
+                        uint32_t is;
+                        c1 += 1;
+                        if (walk(s, so, L, 0.0f, INFINITY, 1, &ts, &is, &nn, &pp)) lam = 0.0f;
+                    }
+                    const float f = ambient + (1.0f - ambient) * lam;
+                    const uint32_t a = s->albedo[idx];
+                    cr = (float)(a & 0xFFu) * (1.0f / 255.0f) * f;
+                    cg = (float)((a >> 8) & 0xFFu) * (1.0f / 255.0f) * f;
+                    cb = (float)((a >> 16) & 0xFFu) * (1.0f / 255.0f) * f;
+                }
+                c2 += nn;
+                c3 += pp;
+                ar += cr;
+                ag += cg;
+                ab += cb;
+            }
+            const float mr = ar * inv_spp, mg = ag * inv_spp, mb = ab * inv_spp;
+            uint8_t* px = out8 + 4u * (size_t)pid;
+            px[0] = (uint8_t)(sat(mr) * 255.0f);
+            px[1] = (uint8_t)(sat(mg) * 255.0f);
+            px[2] = (uint8_t)(sat(mb) * 255.0f);
+            px[3] = 255;
+            if (out32) {
+                float* pf = out32 + 4u * (size_t)pid;
+                pf[0] = mr;
+                pf[1] = mg;
+                pf[2] = mb;
+                pf[3] = 1.0f;
+            }
+        }
+    }
+    if (counters) {
+        counters[0] += c0;
+        counters[1] += c1;
+        counters[2] += c2;
+        counters[3] += c3;
+    }
+}
+
+int orc_max_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}

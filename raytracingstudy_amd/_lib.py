@@ -1,0 +1,154 @@
+"""ctypes binding of the C-ABI in ``include/rt.h`` (``librt_amd.so``).
+
+The shared library is the product: the HIP kernels for gfx950 plus the host
+runtime.  There is no fallback — if the library is missing or fails to load,
+``load()`` raises, and every render entry point raises with the library's own
+error message when a call fails.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librt_amd.so")
+
+RT_OK = 0
+RT_E_INVALID = -1
+RT_E_HIP = -2
+RT_E_NOMEM = -3
+RT_E_NOSCENE = -4
+RT_E_STATE = -5
+
+RT_MODE_COMPAT = 0
+RT_MODE_SCENE = 1
+
+RT_FLAG_JITTER = 1 << 0
+RT_FLAG_NO_JITTER = 1 << 1
+RT_FLAG_RADIANCE = 1 << 2
+RT_FLAG_NO_SHADOWS = 1 << 3
+
+_f3 = ctypes.c_float * 3
+
+
+class RtConfig(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_uint32),
+        ("height", ctypes.c_uint32),
+        ("spp", ctypes.c_uint32),
+        ("seed", ctypes.c_uint32),
+        ("device", ctypes.c_int32),
+        ("mode", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32),
+        ("light_dir", _f3),
+        ("ambient", ctypes.c_float),
+    ]
+
+
+class RtOctreeParams(ctypes.Structure):
+    _fields_ = [
+        ("min", _f3),
+        ("max", _f3),
+        ("resolution", ctypes.c_float),
+        ("max_depth", ctypes.c_uint32),
+        ("leaf_capacity", ctypes.c_uint32),
+    ]
+
+
+class RtStats(ctypes.Structure):
+    _fields_ = [
+        ("primary_rays", ctypes.c_uint64),
+        ("shadow_rays", ctypes.c_uint64),
+        ("nodes_visited", ctypes.c_uint64),
+        ("prims_tested", ctypes.c_uint64),
+        ("ms", ctypes.c_float),
+        ("reserved", ctypes.c_uint32),
+    ]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+
+
+class RtSceneInfo(ctypes.Structure):
+    _fields_ = [
+        ("n_spheres", ctypes.c_uint32),
+        ("n_nodes", ctypes.c_uint32),
+        ("n_leaves", ctypes.c_uint32),
+        ("n_prim_refs", ctypes.c_uint32),
+        ("max_depth", ctypes.c_uint32),
+        ("depth_reached", ctypes.c_uint32),
+        ("node_bytes", ctypes.c_uint32),
+        ("prim_bytes", ctypes.c_uint32),
+        ("build_ms", ctypes.c_double),
+        ("upload_ms", ctypes.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+# every symbol declared in include/rt.h, with (restype, argtypes)
+_P = ctypes.c_void_p
+_u32 = ctypes.c_uint32
+_int = ctypes.c_int
+_fp = ctypes.POINTER(ctypes.c_float)
+SIGNATURES = {
+    "rt_abi_version": (_int, []),
+    "rt_device_count": (_int, []),
+    "rt_config_default": (None, [ctypes.POINTER(RtConfig)]),
+    "rt_octree_params_default": (None, [ctypes.POINTER(RtOctreeParams)]),
+    "rt_create": (_int, [ctypes.POINTER(RtConfig), ctypes.POINTER(_P)]),
+    "rt_destroy": (_int, [_P]),
+    "rt_set_pose": (_int, [_P, _fp]),
+    "rt_set_intrinsic": (_int, [_P, _fp]),
+    "rt_get_camera": (_int, [_P, _fp, _fp]),
+    "rt_resize": (_int, [_P, _u32, _u32]),
+    "rt_resize_intrinsic": (None, [_u32, _u32, _fp]),
+    "rt_set_scene": (_int, [_P, _P, _P, _u32, ctypes.POINTER(RtOctreeParams)]),
+    "rt_set_octree": (_int, [_P, _fp, _fp, ctypes.c_float]),
+    "rt_get_scene_info": (_int, [_P, ctypes.POINTER(RtSceneInfo)]),
+    "rt_generate_spheres": (_int, [_u32, _u32, _P, _P]),
+    "rt_render": (_int, [_P, _P, _P, ctypes.POINTER(RtStats)]),
+    "rt_render_tiles": (_int, [_P, _P, _u32, _u32, _P, _P, ctypes.POINTER(RtStats)]),
+    "rt_unpack_tiles": (_int, [_P, _P, _P, _u32, _u32, _P, _P]),
+    "rt_synchronize": (_int, [_P]),
+    "rt_readback": (_int, [_P, _P, _P]),
+    "rt_framebuffer": (_P, [_P]),
+    "rt_last_error": (ctypes.c_char_p, [_P]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class RtError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"rt error {code}: {msg}")
+        self.code = code
+
+
+def load() -> ctypes.CDLL:
+    """Load librt_amd.so (raises if it is missing: there is no fallback)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                " (or `make -C raytracingstudy_amd/csrc`); the render path has no CPU fallback")
+        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def check(code: int, handle=None) -> None:
+    if code != RT_OK:
+        lib = load()
+        msg = lib.rt_last_error(handle)
+        raise RtError(code, msg.decode() if msg else "")

@@ -1,0 +1,556 @@
+// rt_capi.cpp — the C-ABI (include/rt.h) over the HIP kernels.
+//
+// Host runtime that replaces KernelRenderer (include/renderer.cuh:25-50,
+// src/renderer.cu:111-198): camera/octree state lives on the host and goes to
+// the kernels by value; device buffers are owned here (the reference leaks
+// its device-heap Camera/Octree, src/renderer.cu:189-198); every call returns
+// a status (the reference's render path checks nothing, :145-151).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "../../include/rt.h"
+#include "rt_params.h"
+#include "scene_build.h"
+
+namespace rtamd {
+hipError_t launch_compat(const FrameArgs& a, hipStream_t st);
+hipError_t launch_scene(const FrameArgs& a, hipStream_t st);
+hipError_t launch_unpack(const uint32_t* packed, const uint32_t* tiles, uint32_t n_tiles,
+                         uint32_t ts, uint32_t tiles_x, uint32_t W, uint32_t H, uint32_t* img,
+                         hipStream_t st);
+size_t scene_lds_bytes(uint32_t max_depth);
+}  // namespace rtamd
+
+using namespace rtamd;
+
+namespace {
+thread_local std::string g_last_error;
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;  // elements
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+}  // namespace
+
+struct rt_renderer {
+    rt_config cfg;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float pose[16];
+    float K[9];
+    uint32_t W = 0, H = 0;
+    DevBuf<uint32_t> fb;
+    DevBuf<float4> rad;
+    DevBuf<unsigned long long> counters;
+    DevBuf<uint32_t> tiles;          // tile list for rt_render_tiles
+    std::vector<uint32_t> tiles_host;  // its host copy (source of the async upload)
+    DevBuf<uint32_t> utiles;         // tile list for rt_unpack_tiles
+    std::vector<uint32_t> utiles_host;
+    // scene (host copies + device arrays)
+    std::vector<float> spheres;
+    std::vector<uint32_t> albedo;
+    rt_octree_params oct;
+    bool has_scene = false;
+    DevBuf<uint2> d_nodes;
+    DevBuf<float4> d_prim_sp;
+    DevBuf<uint32_t> d_prim_idx;
+    DevBuf<float4> d_spheres;
+    DevBuf<uint32_t> d_albedo;
+    SceneArgs sc{};
+    rt_scene_info info{};
+    std::string err;
+};
+
+namespace {
+
+int fail(rt_renderer* r, int code, const std::string& msg) {
+    g_last_error = msg;
+    if (r) r->err = msg;
+    return code;
+}
+
+int hip_fail(rt_renderer* r, hipError_t e, const char* what) {
+    std::string m = std::string(what) + ": " + hipGetErrorString(e);
+    return fail(r, RT_E_HIP, m);
+}
+
+#define RT_HIP(r, call)                                   \
+    do {                                                  \
+        hipError_t e_ = (call);                           \
+        if (e_ != hipSuccess) return hip_fail((r), e_, #call); \
+    } while (0)
+
+template <typename T>
+int ensure(rt_renderer* r, DevBuf<T>& b, size_t n) {
+    if (b.n >= n && b.p) return RT_OK;
+    b.release();
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&b.p), n * sizeof(T));
+    if (e != hipSuccess) {
+        b.p = nullptr;
+        return hip_fail(r, e, "hipMalloc");
+    }
+    b.n = n;
+    return RT_OK;
+}
+
+int set_device(rt_renderer* r) {
+    RT_HIP(r, hipSetDevice(r->device));
+    return RT_OK;
+}
+
+void fill_frame_args(rt_renderer* r, FrameArgs& a) {
+    memset(&a, 0, sizeof(a));
+    memcpy(a.cam.K, r->K, sizeof(r->K));
+    for (int c = 0; c < 3; ++c)
+        for (int row = 0; row < 3; ++row) a.cam.R[c * 3 + row] = r->pose[c * 4 + row];
+    a.cam.o[0] = r->pose[12];
+    a.cam.o[1] = r->pose[13];
+    a.cam.o[2] = r->pose[14];
+    a.sc = r->sc;
+    a.W = r->W;
+    a.H = r->H;
+    a.spp = r->cfg.spp ? r->cfg.spp : 1;
+    a.seedmix = mix32(r->cfg.seed ^ 0x9E3779B9u);
+    bool jitter = a.spp > 1;
+    if (r->cfg.flags & RT_FLAG_JITTER) jitter = true;
+    if (r->cfg.flags & RT_FLAG_NO_JITTER) jitter = false;
+    a.jitter = jitter ? 1u : 0u;
+    a.shadows = (r->cfg.flags & RT_FLAG_NO_SHADOWS) ? 0u : 1u;
+    const float* ld = r->cfg.light_dir;
+    const float ll = sqrtf(ld[0] * ld[0] + ld[1] * ld[1] + ld[2] * ld[2]);
+    a.L[0] = -(ld[0] / ll);
+    a.L[1] = -(ld[1] / ll);
+    a.L[2] = -(ld[2] / ll);
+    a.ambient = r->cfg.ambient;
+    a.inv_spp = 1.0f / static_cast<float>(a.spp);
+    a.counters = r->counters.p;
+}
+
+int upload_scene(rt_renderer* r) {
+    const uint32_t n = static_cast<uint32_t>(r->albedo.size());
+    rt_octree_params& p = r->oct;
+    uint32_t depth = p.max_depth ? p.max_depth : depth_for_resolution(p.min, p.max, p.resolution);
+    if (depth > kMaxDepth) depth = kMaxDepth;
+    auto t0 = std::chrono::steady_clock::now();
+    BuiltOctree tree;
+    build_octree(r->spheres.data(), n, p.min, p.max, depth, p.leaf_capacity ? p.leaf_capacity : 8,
+                 tree);
+    auto t1 = std::chrono::steady_clock::now();
+    int st;
+    if ((st = set_device(r))) return st;
+    const size_t nn = tree.nodes.size(), np = tree.prim_idx.size();
+    if ((st = ensure(r, r->d_nodes, nn))) return st;
+    if ((st = ensure(r, r->d_prim_sp, np))) return st;
+    if ((st = ensure(r, r->d_prim_idx, np))) return st;
+    if ((st = ensure(r, r->d_spheres, n))) return st;
+    if ((st = ensure(r, r->d_albedo, n))) return st;
+    RT_HIP(r, hipMemcpy(r->d_nodes.p, tree.nodes.data(), nn * sizeof(uint2), hipMemcpyHostToDevice));
+    if (np) {
+        RT_HIP(r, hipMemcpy(r->d_prim_sp.p, tree.prim_sp.data(), np * sizeof(float4),
+                            hipMemcpyHostToDevice));
+        RT_HIP(r, hipMemcpy(r->d_prim_idx.p, tree.prim_idx.data(), np * sizeof(uint32_t),
+                            hipMemcpyHostToDevice));
+    }
+    if (n) {
+        RT_HIP(r, hipMemcpy(r->d_spheres.p, r->spheres.data(), n * sizeof(float4),
+                            hipMemcpyHostToDevice));
+        RT_HIP(r, hipMemcpy(r->d_albedo.p, r->albedo.data(), n * sizeof(uint32_t),
+                            hipMemcpyHostToDevice));
+    }
+    auto t2 = std::chrono::steady_clock::now();
+
+    SceneArgs& sc = r->sc;
+    sc.nodes = r->d_nodes.p;
+    sc.prim_sp = r->d_prim_sp.p;
+    sc.prim_idx = r->d_prim_idx.p;
+    sc.spheres = r->d_spheres.p;
+    sc.albedo = r->d_albedo.p;
+    sc.root = make_uint2(tree.nodes[0].x, tree.nodes[0].y);
+    sc.root_is_leaf = tree.root_is_leaf ? 1u : 0u;
+    sc.max_depth = depth;
+    sc.G = static_cast<float>(1u << depth);
+    for (int i = 0; i < 3; ++i) {
+        sc.rmin[i] = p.min[i];
+        sc.scale[i] = sc.G / (p.max[i] - p.min[i]);
+    }
+    rt_scene_info& in = r->info;
+    in.n_spheres = n;
+    in.n_nodes = static_cast<uint32_t>(nn);
+    in.n_leaves = tree.n_leaves;
+    in.n_prim_refs = static_cast<uint32_t>(np);
+    in.max_depth = depth;
+    in.depth_reached = tree.depth_reached;
+    in.node_bytes = sizeof(uint2);
+    in.prim_bytes = sizeof(float4) + sizeof(uint32_t);
+    in.build_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    in.upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+    r->has_scene = true;
+    return RT_OK;
+}
+
+int check_tiles(rt_renderer* r, const uint32_t* ids, uint32_t n_tiles, uint32_t ts) {
+    if (ts == 0 || ts % 64 != 0 || ts > 4096)
+        return fail(r, RT_E_INVALID, "tile_size must be a multiple of 64 in [64, 4096]");
+    const uint32_t tx = (r->W + ts - 1) / ts, ty = (r->H + ts - 1) / ts;
+    for (uint32_t i = 0; i < n_tiles; ++i)
+        if (ids[i] >= tx * ty) return fail(r, RT_E_INVALID, "tile id out of range");
+    return RT_OK;
+}
+
+// Upload a tile list only when it changed; the host vector stays alive as the
+// source of the asynchronous copy, so steady-state frames never synchronise.
+int upload_tiles(rt_renderer* r, DevBuf<uint32_t>& dev, std::vector<uint32_t>& host,
+                 const uint32_t* ids, uint32_t n, hipStream_t s) {
+    if (host.size() == n && dev.p && memcmp(host.data(), ids, n * sizeof(uint32_t)) == 0)
+        return RT_OK;
+    int st;
+    if ((st = ensure(r, dev, n))) return st;
+    host.assign(ids, ids + n);
+    RT_HIP(r, hipMemcpyAsync(dev.p, host.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    return RT_OK;
+}
+
+int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : r->stream;
+    if (r->cfg.mode == RT_MODE_SCENE && !r->has_scene)
+        return fail(r, RT_E_NOSCENE, "RT_MODE_SCENE render without rt_set_scene");
+    RT_HIP(r, hipMemsetAsync(r->counters.p, 0, 4 * sizeof(unsigned long long), st));
+    if (stats) RT_HIP(r, hipEventRecord(r->ev0, st));
+    hipError_t e = r->cfg.mode == RT_MODE_SCENE ? launch_scene(a, st) : launch_compat(a, st);
+    if (e != hipSuccess) return hip_fail(r, e, "kernel launch");
+    if (stats) {
+        RT_HIP(r, hipEventRecord(r->ev1, st));
+        RT_HIP(r, hipEventSynchronize(r->ev1));
+        unsigned long long c[4];
+        RT_HIP(r, hipMemcpy(c, r->counters.p, sizeof(c), hipMemcpyDeviceToHost));
+        float ms = 0.f;
+        RT_HIP(r, hipEventElapsedTime(&ms, r->ev0, r->ev1));
+        memset(stats, 0, sizeof(*stats));
+        const uint64_t px = a.tiles ? 0 : (uint64_t)a.W * a.H;
+        stats->primary_rays = r->cfg.mode == RT_MODE_SCENE ? c[0] : px;
+        stats->shadow_rays = c[1];
+        stats->nodes_visited = c[2];
+        stats->prims_tested = c[3];
+        stats->ms = ms;
+    }
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void rt_config_default(rt_config* c) {
+    memset(c, 0, sizeof(*c));
+    c->width = 1280;  // main.cpp:6
+    c->height = 720;
+    c->spp = 1;
+    c->seed = 0x2545F491u;
+    c->device = -1;
+    c->mode = RT_MODE_COMPAT;
+    c->flags = 0;
+    c->light_dir[0] = 1.0f;  // normalize(1,1,-1)
+    c->light_dir[1] = 1.0f;
+    c->light_dir[2] = -1.0f;
+    c->ambient = 0.1f;
+}
+
+void rt_octree_params_default(rt_octree_params* p) {
+    memset(p, 0, sizeof(*p));
+    for (int i = 0; i < 3; ++i) {
+        p->min[i] = 0.0f;   // src/renderer.cu:134
+        p->max[i] = 1.28f;  // src/renderer.cu:135
+    }
+    p->resolution = 0.01f;  // src/renderer.cu:136
+    p->max_depth = 0;
+    p->leaf_capacity = 8;
+}
+
+void rt_resize_intrinsic(uint32_t width, uint32_t height, float K[9]) {
+    // src/renderer.cu:162-170 (float arithmetic, integer cx/cy)
+    const float rad = 80.f * 0.01745329251994329576923690768489f;
+    const float f = static_cast<float>(width) / (2.0f * tanf(rad / 2.0f));
+    for (int i = 0; i < 9; ++i) K[i] = 0.0f;
+    K[0] = f;
+    K[4] = f;
+    K[8] = 1.0f;
+    K[2] = static_cast<float>(width / 2u);
+    K[5] = static_cast<float>(height / 2u);
+}
+
+int rt_create(const rt_config* cfg, rt_renderer** out) {
+    if (!cfg || !out) return fail(nullptr, RT_E_INVALID, "rt_create: null argument");
+    *out = nullptr;
+    if (cfg->width == 0 || cfg->height == 0 || cfg->width > 32768 || cfg->height > 32768)
+        return fail(nullptr, RT_E_INVALID, "rt_create: width/height out of range");
+    if (cfg->mode != RT_MODE_COMPAT && cfg->mode != RT_MODE_SCENE)
+        return fail(nullptr, RT_E_INVALID, "rt_create: unknown mode");
+    rt_renderer* r = new (std::nothrow) rt_renderer();
+    if (!r) return fail(nullptr, RT_E_NOMEM, "rt_create: out of host memory");
+    r->cfg = *cfg;
+    if (r->cfg.spp == 0) r->cfg.spp = 1;
+    int dev = cfg->device;
+    if (dev < 0) {
+        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    }
+    r->device = dev;
+    r->W = cfg->width;
+    r->H = cfg->height;
+    // src/renderer.cu:87-89: K0 = mat3(1000,0,640, 0,1000,340, 0,0,1), pose = mat4(1)
+    const float K0[9] = {1000.f, 0.f, 640.f, 0.f, 1000.f, 340.f, 0.f, 0.f, 1.f};
+    memcpy(r->K, K0, sizeof(K0));
+    for (int i = 0; i < 16; ++i) r->pose[i] = (i % 5 == 0) ? 1.0f : 0.0f;
+    rt_octree_params_default(&r->oct);
+    int st;
+    hipError_t e = hipSetDevice(dev);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&r->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&r->ev1);
+    if (e != hipSuccess) {
+        st = hip_fail(nullptr, e, "rt_create");
+        rt_destroy(r);
+        return st;
+    }
+    if ((st = ensure(r, r->fb, (size_t)r->W * r->H)) ||
+        (st = ensure(r, r->counters, 4))) {
+        g_last_error = r->err;
+        rt_destroy(r);
+        return st;
+    }
+    if (cfg->flags & RT_FLAG_RADIANCE) {
+        if ((st = ensure(r, r->rad, (size_t)r->W * r->H))) {
+            g_last_error = r->err;
+            rt_destroy(r);
+            return st;
+        }
+    }
+    *out = r;
+    return RT_OK;
+}
+
+int rt_destroy(rt_renderer* r) {
+    if (!r) return RT_OK;
+    (void)hipSetDevice(r->device);
+    if (r->stream) (void)hipStreamSynchronize(r->stream);
+    r->fb.release();
+    r->rad.release();
+    r->counters.release();
+    r->tiles.release();
+    r->utiles.release();
+    r->d_nodes.release();
+    r->d_prim_sp.release();
+    r->d_prim_idx.release();
+    r->d_spheres.release();
+    r->d_albedo.release();
+    if (r->ev0) (void)hipEventDestroy(r->ev0);
+    if (r->ev1) (void)hipEventDestroy(r->ev1);
+    if (r->stream) (void)hipStreamDestroy(r->stream);
+    delete r;
+    return RT_OK;
+}
+
+int rt_set_pose(rt_renderer* r, const float pose[16]) {
+    if (!r || !pose) return fail(r, RT_E_INVALID, "rt_set_pose: null argument");
+    memcpy(r->pose, pose, sizeof(r->pose));
+    return RT_OK;
+}
+
+int rt_set_intrinsic(rt_renderer* r, const float K[9]) {
+    if (!r || !K) return fail(r, RT_E_INVALID, "rt_set_intrinsic: null argument");
+    memcpy(r->K, K, sizeof(r->K));
+    return RT_OK;
+}
+
+int rt_get_camera(const rt_renderer* r, float pose_out[16], float K_out[9]) {
+    if (!r) return RT_E_INVALID;
+    if (pose_out) memcpy(pose_out, r->pose, sizeof(r->pose));
+    if (K_out) memcpy(K_out, r->K, sizeof(r->K));
+    return RT_OK;
+}
+
+int rt_resize(rt_renderer* r, uint32_t width, uint32_t height) {
+    if (!r) return fail(r, RT_E_INVALID, "rt_resize: null handle");
+    if (width == 0 || height == 0 || width > 32768 || height > 32768)
+        return fail(r, RT_E_INVALID, "rt_resize: width/height out of range");
+    int st;
+    if ((st = set_device(r))) return st;
+    RT_HIP(r, hipStreamSynchronize(r->stream));
+    r->W = width;
+    r->H = height;
+    if ((st = ensure(r, r->fb, (size_t)width * height))) return st;
+    if (r->cfg.flags & RT_FLAG_RADIANCE)
+        if ((st = ensure(r, r->rad, (size_t)width * height))) return st;
+    rt_resize_intrinsic(width, height, r->K);
+    return RT_OK;
+}
+
+int rt_set_scene(rt_renderer* r, const float* spheres, const uint32_t* albedo, uint32_t n,
+                 const rt_octree_params* oct) {
+    if (!r) return fail(r, RT_E_INVALID, "rt_set_scene: null handle");
+    if (n && !spheres) return fail(r, RT_E_INVALID, "rt_set_scene: null spheres");
+    if (oct) {
+        for (int i = 0; i < 3; ++i)
+            if (!(oct->max[i] > oct->min[i]))
+                return fail(r, RT_E_INVALID, "rt_set_scene: empty octree root box");
+        if (oct->max_depth > kMaxDepth)
+            return fail(r, RT_E_INVALID, "rt_set_scene: max_depth > 16");
+        if (oct->max_depth == 0 && !(oct->resolution > 0.0f))
+            return fail(r, RT_E_INVALID, "rt_set_scene: need max_depth or resolution > 0");
+        r->oct = *oct;
+    }
+    for (uint32_t i = 0; i < n; ++i)
+        if (!(spheres[4 * i + 3] > 0.0f) || !isfinite(spheres[4 * i]) ||
+            !isfinite(spheres[4 * i + 1]) || !isfinite(spheres[4 * i + 2]))
+            return fail(r, RT_E_INVALID, "rt_set_scene: sphere with radius <= 0 or non-finite centre");
+    r->spheres.assign(spheres, spheres + 4u * n);
+    r->albedo.resize(n);
+    for (uint32_t i = 0; i < n; ++i) r->albedo[i] = albedo ? albedo[i] : 0xFFCCCCCCu;
+    return upload_scene(r);
+}
+
+int rt_set_octree(rt_renderer* r, const float mn[3], const float mx[3], float resolution) {
+    if (!r || !mn || !mx) return fail(r, RT_E_INVALID, "rt_set_octree: null argument");
+    rt_octree_params p = r->oct;
+    for (int i = 0; i < 3; ++i) {
+        p.min[i] = mn[i];
+        p.max[i] = mx[i];
+        if (!(mx[i] > mn[i])) return fail(r, RT_E_INVALID, "rt_set_octree: empty box");
+    }
+    if (!(resolution > 0.0f)) return fail(r, RT_E_INVALID, "rt_set_octree: resolution <= 0");
+    p.resolution = resolution;
+    p.max_depth = 0;
+    r->oct = p;
+    if (!r->has_scene && r->spheres.empty()) return RT_OK;
+    return upload_scene(r);
+}
+
+int rt_get_scene_info(const rt_renderer* r, rt_scene_info* info) {
+    if (!r || !info) return RT_E_INVALID;
+    if (!r->has_scene) return RT_E_NOSCENE;
+    *info = r->info;
+    return RT_OK;
+}
+
+int rt_generate_spheres(uint32_t n, uint32_t seed, float* spheres_out, uint32_t* albedo_out) {
+    if (n && !spheres_out) return fail(nullptr, RT_E_INVALID, "rt_generate_spheres: null output");
+    generate_spheres(n, seed, spheres_out, albedo_out);
+    return RT_OK;
+}
+
+int rt_render(rt_renderer* r, void* dev_rgba8, void* stream, rt_stats* stats) {
+    if (!r) return fail(r, RT_E_INVALID, "rt_render: null handle");
+    int st;
+    if ((st = set_device(r))) return st;
+    FrameArgs a;
+    fill_frame_args(r, a);
+    a.out8 = dev_rgba8 ? static_cast<uint32_t*>(dev_rgba8) : r->fb.p;
+    a.out32 = (r->cfg.flags & RT_FLAG_RADIANCE) ? r->rad.p : nullptr;
+    return do_render(r, a, stream, stats);
+}
+
+int rt_render_tiles(rt_renderer* r, const uint32_t* tile_ids, uint32_t n_tiles, uint32_t ts,
+                    void* dev_packed, void* stream, rt_stats* stats) {
+    if (!r) return fail(r, RT_E_INVALID, "rt_render_tiles: null handle");
+    if (n_tiles && (!tile_ids || !dev_packed))
+        return fail(r, RT_E_INVALID, "rt_render_tiles: null argument");
+    int st;
+    if ((st = check_tiles(r, tile_ids, n_tiles, ts))) return st;
+    const uint32_t tx = (r->W + ts - 1) / ts;
+    if ((st = set_device(r))) return st;
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->stream;
+    if (n_tiles == 0) {
+        if (stats) memset(stats, 0, sizeof(*stats));
+        return RT_OK;
+    }
+    if ((st = upload_tiles(r, r->tiles, r->tiles_host, tile_ids, n_tiles, s))) return st;
+    FrameArgs a;
+    fill_frame_args(r, a);
+    a.out8 = static_cast<uint32_t*>(dev_packed);
+    a.out32 = nullptr;
+    a.tiles = r->tiles.p;
+    a.n_tiles = n_tiles;
+    a.tile_size = ts;
+    a.tiles_x = tx;
+    st = do_render(r, a, s, stats);
+    if (!st && stats && r->cfg.mode != RT_MODE_SCENE) {
+        uint64_t px = 0;
+        for (uint32_t i = 0; i < n_tiles; ++i) {
+            const uint32_t x0 = (tile_ids[i] % tx) * ts, y0 = (tile_ids[i] / tx) * ts;
+            const uint64_t w = std::min<uint64_t>(ts, r->W - x0), h = std::min<uint64_t>(ts, r->H - y0);
+            px += w * h;
+        }
+        stats->primary_rays = px;
+    }
+    return st;
+}
+
+int rt_unpack_tiles(rt_renderer* r, const void* dev_packed, const uint32_t* tile_ids,
+                    uint32_t n_tiles, uint32_t ts, void* dev_rgba8, void* stream) {
+    if (!r) return fail(r, RT_E_INVALID, "rt_unpack_tiles: null handle");
+    if (n_tiles && (!tile_ids || !dev_packed)) return fail(r, RT_E_INVALID, "rt_unpack_tiles: null argument");
+    int st;
+    if ((st = check_tiles(r, tile_ids, n_tiles, ts))) return st;
+    if (n_tiles == 0) return RT_OK;
+    const uint32_t tx = (r->W + ts - 1) / ts;
+    if ((st = set_device(r))) return st;
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->stream;
+    if ((st = upload_tiles(r, r->utiles, r->utiles_host, tile_ids, n_tiles, s))) return st;
+    hipError_t e = launch_unpack(static_cast<const uint32_t*>(dev_packed), r->utiles.p, n_tiles, ts, tx,
+                                 r->W, r->H, dev_rgba8 ? static_cast<uint32_t*>(dev_rgba8) : r->fb.p, s);
+    if (e != hipSuccess) return hip_fail(r, e, "rt_unpack_tiles");
+    return RT_OK;
+}
+
+int rt_synchronize(rt_renderer* r) {
+    if (!r) return RT_E_INVALID;
+    int st;
+    if ((st = set_device(r))) return st;
+    RT_HIP(r, hipStreamSynchronize(r->stream));
+    return RT_OK;
+}
+
+int rt_readback(rt_renderer* r, uint8_t* host_rgba8, float* host_rgba32f) {
+    if (!r) return RT_E_INVALID;
+    int st;
+    if ((st = set_device(r))) return st;
+    RT_HIP(r, hipStreamSynchronize(r->stream));
+    const size_t px = (size_t)r->W * r->H;
+    if (host_rgba8) RT_HIP(r, hipMemcpy(host_rgba8, r->fb.p, px * 4, hipMemcpyDeviceToHost));
+    if (host_rgba32f) {
+        if (!(r->cfg.flags & RT_FLAG_RADIANCE))
+            return fail(r, RT_E_STATE, "rt_readback: radiance buffer needs RT_FLAG_RADIANCE");
+        RT_HIP(r, hipMemcpy(host_rgba32f, r->rad.p, px * 16, hipMemcpyDeviceToHost));
+    }
+    return RT_OK;
+}
+
+void* rt_framebuffer(rt_renderer* r) { return r ? r->fb.p : nullptr; }
+
+const char* rt_last_error(const rt_renderer* r) {
+    if (r) return r->err.c_str();
+    return g_last_error.c_str();
+}
+
+}  // extern "C"

@@ -1,0 +1,68 @@
+// rt_params.h — kernel-argument structs shared by the C-ABI host code and the
+// HIP kernels.  Everything the hot loop needs travels BY VALUE in one kernel
+// argument block (SGPR-resident), replacing the reference's device-heap
+// Camera/Octree objects reached through thrust::device_ptr<T*> double
+// indirection (src/renderer.cu:57,65-66,84-109).
+#pragma once
+#include <stdint.h>
+
+namespace rtamd {
+
+constexpr int kBlockThreads = 256;  // 4 waves of 64
+constexpr int kTileSide = 16;       // scene kernel: 16x16 pixels per workgroup, 8x8 per wave
+constexpr uint32_t kMaxDepth = 16;  // octree depth limit (grid coordinates stay < 2^16, exact in f32)
+constexpr float kShadowEps = 1e-5f; // shadow-ray origin offset along the normal (world units)
+constexpr uint32_t kNoHit = 0xFFFFFFFFu;
+
+// Pinhole camera (include/camera.h:9-56): K and R column-major like glm.
+struct CamArgs {
+    float K[9];  // K[c*3+r]
+    float R[9];  // rot = mat3(pose): R[c*3+r] = pose[c*4+r]
+    float o[3];  // origin = pose[3].xyz
+};
+
+// Octree in HBM (DESIGN.md "Data layout"):
+//   nodes[]   : uint2 records.  internal: {first child slot, valid | leaf<<8}
+//                               leaf    : {first prim ref, prim count}
+//               children of a node occupy consecutive slots, only the valid
+//               ones, in real child order (bit0 x, bit1 y, bit2 z);
+//               breadth-first, so the top levels are contiguous.
+//   prim_sp[] : float4 (cx, cy, cz, r), one per leaf reference (leaf-contiguous)
+//   prim_idx[]: sphere index of each reference (nearest-hit tie-break, shading)
+struct SceneArgs {
+    const uint2* nodes;
+    const float4* prim_sp;
+    const uint32_t* prim_idx;
+    const float4* spheres;   // by sphere index (shading)
+    const uint32_t* albedo;  // packed RGBA8 by sphere index
+    uint2 root;              // nodes[0], also passed by value
+    uint32_t root_is_leaf;
+    uint32_t max_depth;      // D: grid is G = 2^D cells per axis
+    float rmin[3];
+    float scale[3];          // G / (rmax - rmin), f32
+    float G;
+};
+
+struct FrameArgs {
+    CamArgs cam;
+    SceneArgs sc;
+    uint32_t W, H;
+    uint32_t spp;
+    uint32_t seedmix;   // mix32(seed ^ 0x9E3779B9)
+    uint32_t jitter;
+    uint32_t shadows;
+    float L[3];         // unit vector toward the light
+    float ambient;
+    float inv_spp;
+    // output
+    uint32_t* out8;     // RGBA8 (R in the low byte), frame- or tile-packed
+    float4* out32;      // optional mean radiance (frame layout only), may be null
+    // tile mode (out8 packed per tile)
+    const uint32_t* tiles;
+    uint32_t n_tiles;
+    uint32_t tile_size;
+    uint32_t tiles_x;   // ceil(W / tile_size)
+    unsigned long long* counters;  // [primary, shadow, nodes, prims]
+};
+
+}  // namespace rtamd

@@ -1,0 +1,196 @@
+// scene_build.cpp — host-side scene generator + breadth-first octree builder.
+//
+// The reference has no primitives and no octree structure: Octree holds only
+// its bounds and `resolution` (include/octree.h:7-23, constructed with
+// min 0, max 1.28, resolution 0.01 at src/renderer.cu:134-138) and traverse()
+// is a stub.  This builder defines the structure the render kernel walks;
+// the semantics are specified in DESIGN.md "Octree build".
+#include "scene_build.h"
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+
+namespace rtamd {
+
+uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+namespace {
+
+uint64_t splitmix64(uint64_t& x) {
+    uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+struct Pcg32 {
+    uint64_t state, inc;
+    uint32_t next() {
+        const uint64_t old = state;
+        state = old * 6364136223846793005ull + inc;
+        const uint32_t xs = static_cast<uint32_t>(((old >> 18u) ^ old) >> 27u);
+        const uint32_t rot = static_cast<uint32_t>(old >> 59u);
+        return (xs >> rot) | (xs << ((0u - rot) & 31u));
+    }
+    float unit() { return static_cast<float>(next() >> 8) * (1.0f / 16777216.0f); }
+};
+
+struct Cell {
+    uint32_t depth;
+    uint32_t c[3];
+    uint32_t slot;               // index of this node's record in nodes[]
+    std::vector<uint32_t> list;  // sphere indices, ascending
+};
+
+struct Geometry {
+    double lo[3], ext[3];
+    double margin;
+    void bounds(uint32_t depth, const uint32_t c[3], double blo[3], double bhi[3]) const {
+        const double cells = static_cast<double>(1u << depth);
+        for (int i = 0; i < 3; ++i) {
+            blo[i] = lo[i] + ext[i] * (static_cast<double>(c[i]) / cells);
+            bhi[i] = lo[i] + ext[i] * (static_cast<double>(c[i] + 1u) / cells);
+        }
+    }
+    bool overlaps(const float* sp, const double blo[3], const double bhi[3]) const {
+        double d2 = 0.0;
+        for (int i = 0; i < 3; ++i) {
+            const double c = static_cast<double>(sp[i]);
+            if (c < blo[i]) {
+                const double e = blo[i] - c;
+                d2 += e * e;
+            } else if (c > bhi[i]) {
+                const double e = c - bhi[i];
+                d2 += e * e;
+            }
+        }
+        const double r = static_cast<double>(sp[3]) + margin;
+        return d2 <= r * r;
+    }
+};
+
+}  // namespace
+
+void generate_spheres(uint32_t n, uint32_t seed, float* sp, uint32_t* albedo) {
+    uint64_t sm = seed;
+    Pcg32 g;
+    g.state = splitmix64(sm);
+    g.inc = splitmix64(sm) | 1ull;
+    const float rscale = n ? static_cast<float>(0.02 * cbrt(1000.0 / static_cast<double>(n))) : 0.0f;
+    for (uint32_t i = 0; i < n; ++i) {
+        const float cx = g.unit() * 1.28f;
+        const float cy = g.unit() * 1.28f;
+        const float cz = g.unit() * 1.28f;
+        const float ru = g.unit();
+        sp[4 * i + 0] = cx;
+        sp[4 * i + 1] = cy;
+        sp[4 * i + 2] = cz;
+        sp[4 * i + 3] = rscale * (0.5f + 0.5f * ru);
+        uint32_t a = 0xFF000000u;
+        for (int c = 0; c < 3; ++c) {
+            const float v = 0.2f + 0.8f * g.unit();
+            a |= (static_cast<uint32_t>(v * 255.0f) & 0xFFu) << (8 * c);
+        }
+        if (albedo) albedo[i] = a;
+    }
+}
+
+uint32_t depth_for_resolution(const float rmin[3], const float rmax[3], float res) {
+    float ext = 0.0f;
+    for (int i = 0; i < 3; ++i) ext = std::max(ext, rmax[i] - rmin[i]);
+    if (!(res > 0.0f)) return 7;
+    uint32_t d = 0;
+    while (d < 16 && static_cast<double>(ext) / static_cast<double>(1u << d) >
+                         static_cast<double>(res) * (1.0 + 1e-6))
+        ++d;
+    return d;
+}
+
+void build_octree(const float* spheres, uint32_t n, const float rmin[3], const float rmax[3],
+                  uint32_t max_depth, uint32_t leaf_cap, BuiltOctree& out) {
+    out = BuiltOctree();
+    Geometry geo;
+    double m = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        geo.lo[i] = static_cast<double>(rmin[i]);
+        geo.ext[i] = static_cast<double>(rmax[i]) - static_cast<double>(rmin[i]);
+        m = std::max(m, geo.ext[i]);
+    }
+    geo.margin = 1e-6 * m;
+
+    Cell root;
+    root.depth = 0;
+    root.c[0] = root.c[1] = root.c[2] = 0;
+    root.slot = 0;
+    {
+        double blo[3], bhi[3];
+        geo.bounds(0, root.c, blo, bhi);
+        for (uint32_t i = 0; i < n; ++i)
+            if (geo.overlaps(spheres + 4u * i, blo, bhi)) root.list.push_back(i);
+    }
+    out.nodes.push_back({0, 0});
+
+    auto is_leaf = [&](const Cell& c) {
+        return c.list.size() <= leaf_cap || c.depth >= max_depth;
+    };
+    out.root_is_leaf = is_leaf(root);
+
+    // Breadth-first: `level` holds the cells of one depth in slot order, so
+    // every node's children are appended as one contiguous block.
+    std::vector<Cell> level;
+    level.push_back(std::move(root));
+    std::vector<uint32_t> sub;
+    while (!level.empty()) {
+        std::vector<Cell> next;
+        for (Cell& cell : level) {
+            if (is_leaf(cell)) {
+                const uint32_t off = static_cast<uint32_t>(out.prim_idx.size());
+                for (uint32_t idx : cell.list) {
+                    out.prim_idx.push_back(idx);
+                    out.prim_sp.insert(out.prim_sp.end(), spheres + 4u * idx, spheres + 4u * idx + 4);
+                }
+                out.nodes[cell.slot] = {off, static_cast<uint32_t>(cell.list.size())};
+                out.n_leaves++;
+                out.depth_reached = std::max(out.depth_reached, cell.depth);
+                continue;
+            }
+            uint32_t valid = 0, leafm = 0;
+            Cell kids[8];
+            for (uint32_t ch = 0; ch < 8; ++ch) {
+                Cell& k = kids[ch];
+                k.depth = cell.depth + 1;
+                k.c[0] = 2 * cell.c[0] + (ch & 1u);
+                k.c[1] = 2 * cell.c[1] + ((ch >> 1) & 1u);
+                k.c[2] = 2 * cell.c[2] + ((ch >> 2) & 1u);
+                double blo[3], bhi[3];
+                geo.bounds(k.depth, k.c, blo, bhi);
+                for (uint32_t idx : cell.list)
+                    if (geo.overlaps(spheres + 4u * idx, blo, bhi)) k.list.push_back(idx);
+                if (k.list.empty()) continue;
+                valid |= 1u << ch;
+                if (is_leaf(k)) leafm |= 1u << ch;
+            }
+            const uint32_t first = static_cast<uint32_t>(out.nodes.size());
+            out.nodes[cell.slot] = {first, valid | (leafm << 8)};
+            for (uint32_t ch = 0; ch < 8; ++ch) {
+                if (!(valid & (1u << ch))) continue;
+                kids[ch].slot = static_cast<uint32_t>(out.nodes.size());
+                out.nodes.push_back({0, 0});
+                next.push_back(std::move(kids[ch]));
+            }
+            std::vector<uint32_t>().swap(cell.list);
+        }
+        level.swap(next);
+    }
+}
+
+}  // namespace rtamd

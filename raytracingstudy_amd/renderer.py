@@ -1,0 +1,216 @@
+"""Host-side mirror of the reference's ``KernelRenderer`` over the C-ABI.
+
+Reference interface (``include/renderer.cuh:25-50``)::
+
+    KernelRenderer(cudaGraphicsResource_t cudaResource, int width, int height);
+    void render();
+    void resize(int width, int height);
+    void setPosition(glm::mat4 pose);
+    void setIntrinsic(glm::mat3 intrinsic);
+    void setOctree(glm::vec3 min, glm::vec3 max, float resolution);
+
+This class keeps those method names, argument meanings (glm column-major
+matrices, pixel units) and call order, and adds what the reference left as
+stubs: a real scene (``set_scene``), tiles for multi-GPU sharding, stats and
+error reporting (the reference's methods return ``void`` and check nothing;
+here a failing call raises ``RtError`` with the library's message).
+
+Matrices are given in glm indexing: ``pose[c][r]`` is glm's ``m[c][r]`` (column
+``c``, row ``r``), so ``pose[3][:3]`` is the camera origin
+(``include/camera.h:43-46``) and ``K[0][2]``/``K[1][2]`` are cx/cy
+(``include/camera.h:26-27``).  Flattening in C order yields glm's memory layout.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import (RT_FLAG_JITTER, RT_FLAG_NO_JITTER, RT_FLAG_NO_SHADOWS, RT_FLAG_RADIANCE,
+                   RT_MODE_COMPAT, RT_MODE_SCENE, RtConfig, RtOctreeParams, RtSceneInfo,
+                   RtStats, check)
+
+__all__ = ["KernelRenderer", "resize_intrinsic", "generate_spheres", "device_count"]
+
+_MODES = {"compat": RT_MODE_COMPAT, "scene": RT_MODE_SCENE}
+
+
+def _fptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _vptr(a: Optional[np.ndarray]):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def device_count() -> int:
+    return int(_lib.load().rt_device_count())
+
+
+def resize_intrinsic(width: int, height: int) -> np.ndarray:
+    """K the reference's resize() sets (src/renderer.cu:162-170), glm [c][r] indexing."""
+    K = np.zeros(9, np.float32)
+    _lib.load().rt_resize_intrinsic(width, height, _fptr(K))
+    return K.reshape(3, 3)
+
+
+def generate_spheres(n: int, seed: int = 0x2545F491):
+    """SURVEY.md 8d synthetic spheres: (n,4) float32 (cx,cy,cz,r) and (n,) uint32 albedo."""
+    sp = np.zeros((max(n, 1), 4), np.float32)
+    al = np.zeros(max(n, 1), np.uint32)
+    check(_lib.load().rt_generate_spheres(n, seed, _vptr(sp), _vptr(al)))
+    return sp[:n], al[:n]
+
+
+class KernelRenderer:
+    """MI355X renderer handle (one per thread / stream)."""
+
+    def __init__(self, width: int, height: int, *, mode: str = "compat", spp: int = 1,
+                 seed: int = 0x2545F491, device: int = -1, jitter: Optional[bool] = None,
+                 shadows: bool = True, radiance: bool = False,
+                 light_dir: Sequence[float] = (1.0, 1.0, -1.0), ambient: float = 0.1):
+        lib = _lib.load()
+        cfg = RtConfig()
+        lib.rt_config_default(ctypes.byref(cfg))
+        cfg.width, cfg.height = int(width), int(height)
+        cfg.spp = int(spp)
+        cfg.seed = int(seed) & 0xFFFFFFFF
+        cfg.device = int(device)
+        cfg.mode = _MODES[mode]
+        flags = 0
+        if jitter is True:
+            flags |= RT_FLAG_JITTER
+        elif jitter is False:
+            flags |= RT_FLAG_NO_JITTER
+        if not shadows:
+            flags |= RT_FLAG_NO_SHADOWS
+        if radiance:
+            flags |= RT_FLAG_RADIANCE
+        cfg.flags = flags
+        for i in range(3):
+            cfg.light_dir[i] = float(light_dir[i])
+        cfg.ambient = float(ambient)
+        self._lib = lib
+        self.config = cfg
+        self.mode = mode
+        self.radiance = radiance
+        h = ctypes.c_void_p()
+        check(lib.rt_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        self.width, self.height = int(width), int(height)
+
+    # -- reference method names -------------------------------------------------
+    def render(self, dev_ptr: Optional[int] = None, stream: Optional[int] = None,
+               stats: bool = False) -> Optional[RtStats]:
+        """render() (src/renderer.cu:143-153).  dev_ptr: a device RGBA8 buffer
+        (e.g. the mapped GL PBO pointer) or None for the internal framebuffer."""
+        st = RtStats() if stats else None
+        check(self._lib.rt_render(self._h, ctypes.c_void_p(dev_ptr) if dev_ptr else None,
+                                  ctypes.c_void_p(stream) if stream else None,
+                                  ctypes.byref(st) if st is not None else None), self._h)
+        return st
+
+    def resize(self, width: int, height: int) -> None:
+        """resize() (src/renderer.cu:155-187): new size + the FOV-80 intrinsic."""
+        check(self._lib.rt_resize(self._h, int(width), int(height)), self._h)
+        self.width, self.height = int(width), int(height)
+
+    def setPosition(self, pose) -> None:
+        """setPosition(glm::mat4) (src/renderer.cu:111-113, include/camera.h:43-46)."""
+        p = np.ascontiguousarray(np.asarray(pose, np.float32).reshape(16))
+        check(self._lib.rt_set_pose(self._h, _fptr(p)), self._h)
+
+    def setIntrinsic(self, K) -> None:
+        """setIntrinsic(glm::mat3) (src/renderer.cu:115-117)."""
+        k = np.ascontiguousarray(np.asarray(K, np.float32).reshape(9))
+        check(self._lib.rt_set_intrinsic(self._h, _fptr(k)), self._h)
+
+    def setOctree(self, mn, mx, resolution: float) -> None:
+        """setOctree(min, max, resolution) (include/renderer.cuh:35; undefined in
+        the reference).  Rebuilds the octree of the current spheres."""
+        a = np.asarray(mn, np.float32).reshape(3).copy()
+        b = np.asarray(mx, np.float32).reshape(3).copy()
+        check(self._lib.rt_set_octree(self._h, _fptr(a), _fptr(b), float(resolution)), self._h)
+
+    # -- additions ------------------------------------------------------------
+    def set_scene(self, spheres: np.ndarray, albedo: Optional[np.ndarray] = None, *,
+                  root_min=(0.0, 0.0, 0.0), root_max=(1.28, 1.28, 1.28),
+                  resolution: float = 0.01, max_depth: int = 0, leaf_capacity: int = 8) -> dict:
+        sp = np.ascontiguousarray(spheres, np.float32).reshape(-1, 4)
+        al = None if albedo is None else np.ascontiguousarray(albedo, np.uint32).reshape(-1)
+        if al is not None and al.shape[0] != sp.shape[0]:
+            raise ValueError("albedo must have one entry per sphere")
+        p = RtOctreeParams()
+        for i in range(3):
+            p.min[i] = float(root_min[i])
+            p.max[i] = float(root_max[i])
+        p.resolution = float(resolution)
+        p.max_depth = int(max_depth)
+        p.leaf_capacity = int(leaf_capacity)
+        check(self._lib.rt_set_scene(self._h, _vptr(sp), _vptr(al), sp.shape[0], ctypes.byref(p)),
+              self._h)
+        return self.scene_info()
+
+    def scene_info(self) -> dict:
+        info = RtSceneInfo()
+        check(self._lib.rt_get_scene_info(self._h, ctypes.byref(info)), self._h)
+        return info.as_dict()
+
+    def camera(self):
+        pose = np.zeros(16, np.float32)
+        K = np.zeros(9, np.float32)
+        check(self._lib.rt_get_camera(self._h, _fptr(pose), _fptr(K)), self._h)
+        return pose.reshape(4, 4), K.reshape(3, 3)
+
+    def render_tiles(self, tile_ids, tile_size: int, dev_ptr: int, stream: Optional[int] = None,
+                     stats: bool = False) -> Optional[RtStats]:
+        ids = np.ascontiguousarray(tile_ids, np.uint32)
+        st = RtStats() if stats else None
+        check(self._lib.rt_render_tiles(self._h, _vptr(ids), ids.shape[0], int(tile_size),
+                                        ctypes.c_void_p(dev_ptr),
+                                        ctypes.c_void_p(stream) if stream else None,
+                                        ctypes.byref(st) if st is not None else None), self._h)
+        return st
+
+    def unpack_tiles(self, dev_packed: int, tile_ids, tile_size: int,
+                     dev_rgba8: Optional[int] = None, stream: Optional[int] = None) -> None:
+        ids = np.ascontiguousarray(tile_ids, np.uint32)
+        check(self._lib.rt_unpack_tiles(self._h, ctypes.c_void_p(dev_packed), _vptr(ids),
+                                        ids.shape[0], int(tile_size),
+                                        ctypes.c_void_p(dev_rgba8) if dev_rgba8 else None,
+                                        ctypes.c_void_p(stream) if stream else None), self._h)
+
+    def synchronize(self) -> None:
+        check(self._lib.rt_synchronize(self._h), self._h)
+
+    def readback(self) -> np.ndarray:
+        out = np.zeros((self.height, self.width, 4), np.uint8)
+        check(self._lib.rt_readback(self._h, _vptr(out), None), self._h)
+        return out
+
+    def readback_radiance(self) -> np.ndarray:
+        out = np.zeros((self.height, self.width, 4), np.float32)
+        check(self._lib.rt_readback(self._h, None, _vptr(out)), self._h)
+        return out
+
+    def framebuffer_ptr(self) -> int:
+        return int(self._lib.rt_framebuffer(self._h) or 0)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.rt_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
