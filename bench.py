@@ -109,7 +109,7 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
-    assert sptr, "need a non-null HIP stream handle
+    assert sptr, "need a non-null HIP stream handle"
     W, H, ts = cfg.width, cfg.height, rt.configs.TILE_SIZE
     frame = torch.empty(W * H * 4, dtype=torch.uint8, device=dev)
     if world > 1:
