@@ -120,6 +120,8 @@ typedef struct rt_scene_info {
     uint32_t depth_reached;  /* deepest leaf                                            */
     uint32_t node_bytes;     /* sizeof one node record                                  */
     uint32_t prim_bytes;     /* bytes read per sphere test                              */
+    float root_min[3];       /* effective root box: the configured box grown to          */
+    float root_max[3];       /*   enclose every sphere (equal to it when none protrudes)  */
     double build_ms;         /* host build time                                         */
     double upload_ms;        /* host->device upload time                                */
 } rt_scene_info;

@@ -43,6 +43,7 @@ def load() -> ctypes.CDLL:
         "orc_scene_free": (None, [_P]),
         "orc_scene_info": (None, [_P, _P]),
         "orc_depth_for_resolution": (_u32, [_P, _P, _f]),
+        "orc_scene_root": (None, [_P, _P, _P]),
         "orc_trace": (ctypes.c_int, [_P, _P, _P, _f, _f, ctypes.c_int, _P, _P, _P]),
         "orc_trace_brute": (ctypes.c_int, [_P, _P, _P, _f, _f, ctypes.c_int, _P, _P]),
         "orc_render_scene": (None, [_P, _u32, _u32, _P, _P, _u32, _u32, _u32, _P, _f, _u32, _u32,
@@ -76,13 +77,15 @@ def resize_intrinsic(w: int, h: int) -> np.ndarray:
 
 def render_compat(w: int, h: int, pose, K) -> np.ndarray:
     out = np.zeros((h, w, 4), np.uint8)
-    load().orc_render_compat(w, h, _p(_f32(pose, 16)), _p(_f32(K, 9)), _p(out))
+    p, k = _f32(pose, 16), _f32(K, 9)  # keep the arrays alive across the call
+    load().orc_render_compat(w, h, _p(p), _p(k), _p(out))
     return out
 
 
 def get_ray(pose, K, u: float, v: float) -> np.ndarray:
     d = np.zeros(3, np.float32)
-    load().orc_get_ray(_p(_f32(pose, 16)), _p(_f32(K, 9)), u, v, _p(d))
+    p, k = _f32(pose, 16), _f32(K, 9)
+    load().orc_get_ray(_p(p), _p(k), u, v, _p(d))
     return d
 
 
@@ -113,16 +116,23 @@ class Scene:
         return {"n_nodes": int(a[0]), "n_leaves": int(a[1]), "n_prim_refs": int(a[2]),
                 "depth_reached": int(a[3])}
 
+    def root(self):
+        a = np.zeros(3, np.float32)
+        b = np.zeros(3, np.float32)
+        load().orc_scene_root(self._h, _p(a), _p(b))
+        return a, b
+
     def trace(self, o, d, tmin=0.0, tmax=float("inf"), any_hit=False, brute=False):
         lib = load()
         t = ctypes.c_float()
         i = ctypes.c_uint32()
         cnt = np.zeros(4, np.uint64)
+        oa, da = _f32(o, 3), _f32(d, 3)  # keep the arrays alive across the call
         if brute:
-            h = lib.orc_trace_brute(self._h, _p(_f32(o, 3)), _p(_f32(d, 3)), tmin, tmax,
+            h = lib.orc_trace_brute(self._h, _p(oa), _p(da), tmin, tmax,
                                     int(any_hit), ctypes.byref(t), ctypes.byref(i))
         else:
-            h = lib.orc_trace(self._h, _p(_f32(o, 3)), _p(_f32(d, 3)), tmin, tmax, int(any_hit),
+            h = lib.orc_trace(self._h, _p(oa), _p(da), tmin, tmax, int(any_hit),
                               ctypes.byref(t), ctypes.byref(i), _p(cnt))
         return (bool(h), t.value, i.value, cnt)
 
@@ -137,8 +147,9 @@ class Scene:
         out8 = np.zeros((h, w, 4), np.uint8)
         out32 = np.zeros((h, w, 4), np.float32) if radiance else None
         cnt = np.zeros(4, np.uint64)
-        load().orc_render_scene(self._h, w, h, _p(_f32(pose, 16)), _p(_f32(K, 9)), spp, seed,
-                                flags, _p(_f32(light_dir, 3)), ambient, x0, y0, x1, y1,
+        pa, ka, la = _f32(pose, 16), _f32(K, 9), _f32(light_dir, 3)  # alive across the call
+        load().orc_render_scene(self._h, w, h, _p(pa), _p(ka), spp, seed,
+                                flags, _p(la), ambient, x0, y0, x1, y1,
                                 row_step, row_phase, _p(out8), _p(out32), _p(cnt), n_threads)
         return out8, out32, cnt
 

@@ -307,14 +307,28 @@ orc_scene* orc_scene_build(const float* spheres, const uint32_t* albedo, uint32_
     s->spheres = s->sp;
     s->albedo = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
     for (uint32_t i = 0; i < n; ++i) s->albedo[i] = albedo ? albedo[i] : 0xFFCCCCCCu;
+    /* Effective root: the configured box, grown (only where needed, by a
+     * margin) to enclose every sphere's AABB, so protruding spheres stay
+     * reachable by the walk. */
+    double um = 0.0;
     for (int i = 0; i < 3; ++i) {
-        s->rmin[i] = root_min[i];
-        s->rmax[i] = root_max[i];
+        const double e = (double)root_max[i] - (double)root_min[i];
+        if (e > um) um = e;
+    }
+    for (int i = 0; i < 3; ++i) {
+        double lo = (double)root_min[i], hi = (double)root_max[i];
+        for (uint32_t k = 0; k < n; ++k) {
+            const double c = (double)spheres[4 * k + i], r = (double)spheres[4 * k + 3];
+            if (c - r < lo) lo = c - r;
+            if (c + r > hi) hi = c + r;
+        }
+        s->rmin[i] = lo < (double)root_min[i] ? (float)(lo - 1e-6 * um) : root_min[i];
+        s->rmax[i] = hi > (double)root_max[i] ? (float)(hi + 1e-6 * um) : root_max[i];
     }
     s->max_depth = max_depth > 16 ? 16 : max_depth;
     s->leaf_cap = leaf_capacity;
     s->G = (float)(1u << s->max_depth);
-    for (int i = 0; i < 3; ++i) s->scale[i] = s->G / (root_max[i] - root_min[i]);
+    for (int i = 0; i < 3; ++i) s->scale[i] = s->G / (s->rmax[i] - s->rmin[i]);
 
     const double margin = margin_of(s);
     const uint32_t zero[3] = {0, 0, 0};
@@ -344,6 +358,13 @@ void orc_scene_info(const orc_scene* s, uint32_t info[4]) {
     info[1] = s->n_leaves;
     info[2] = s->n_prims;
     info[3] = s->depth_reached;
+}
+
+void orc_scene_root(const orc_scene* s, float rmin[3], float rmax[3]) {
+    for (int i = 0; i < 3; ++i) {
+        rmin[i] = s->rmin[i];
+        rmax[i] = s->rmax[i];
+    }
 }
 
 /* ---- ray / sphere ---------------------------------------------------------- */

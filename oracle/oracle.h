@@ -41,6 +41,8 @@ orc_scene* orc_scene_build(const float* spheres, const uint32_t* albedo, uint32_
 void orc_scene_free(orc_scene* s);
 /* info[0]=nodes (internal+leaf), [1]=leaves, [2]=prim refs, [3]=deepest leaf */
 void orc_scene_info(const orc_scene* s, uint32_t info[4]);
+/* effective root box (configured box grown to enclose every sphere) */
+void orc_scene_root(const orc_scene* s, float rmin[3], float rmax[3]);
 uint32_t orc_depth_for_resolution(const float root_min[3], const float root_max[3], float res);
 
 /* counters[0]=primary rays, [1]=shadow rays, [2]=nodes visited, [3]=prims tested */

@@ -80,12 +80,17 @@ class RtSceneInfo(ctypes.Structure):
         ("depth_reached", ctypes.c_uint32),
         ("node_bytes", ctypes.c_uint32),
         ("prim_bytes", ctypes.c_uint32),
+        ("root_min", _f3),
+        ("root_max", _f3),
         ("build_ms", ctypes.c_double),
         ("upload_ms", ctypes.c_double),
     ]
 
     def as_dict(self) -> dict:
-        return {f: getattr(self, f) for f, _ in self._fields_}
+        d = {f: getattr(self, f) for f, _ in self._fields_}
+        d["root_min"] = list(self.root_min)
+        d["root_max"] = list(self.root_max)
+        return d
 
 
 # every symbol declared in include/rt.h, with (restype, argtypes)

@@ -184,8 +184,10 @@ int upload_scene(rt_renderer* r) {
     sc.max_depth = depth;
     sc.G = static_cast<float>(1u << depth);
     for (int i = 0; i < 3; ++i) {
-        sc.rmin[i] = p.min[i];
-        sc.scale[i] = sc.G / (p.max[i] - p.min[i]);
+        sc.rmin[i] = tree.rmin[i];
+        sc.scale[i] = sc.G / (tree.rmax[i] - tree.rmin[i]);
+        r->info.root_min[i] = tree.rmin[i];
+        r->info.root_max[i] = tree.rmax[i];
     }
     rt_scene_info& in = r->info;
     in.n_spheres = n;

@@ -118,11 +118,25 @@ uint32_t depth_for_resolution(const float rmin[3], const float rmax[3], float re
 void build_octree(const float* spheres, uint32_t n, const float rmin[3], const float rmax[3],
                   uint32_t max_depth, uint32_t leaf_cap, BuiltOctree& out) {
     out = BuiltOctree();
+    double um = 0.0;
+    for (int i = 0; i < 3; ++i)
+        um = std::max(um, static_cast<double>(rmax[i]) - static_cast<double>(rmin[i]));
+    for (int i = 0; i < 3; ++i) {
+        double lo = static_cast<double>(rmin[i]), hi = static_cast<double>(rmax[i]);
+        for (uint32_t k = 0; k < n; ++k) {
+            const double c = static_cast<double>(spheres[4 * k + i]);
+            const double r = static_cast<double>(spheres[4 * k + 3]);
+            lo = std::min(lo, c - r);
+            hi = std::max(hi, c + r);
+        }
+        out.rmin[i] = lo < static_cast<double>(rmin[i]) ? static_cast<float>(lo - 1e-6 * um) : rmin[i];
+        out.rmax[i] = hi > static_cast<double>(rmax[i]) ? static_cast<float>(hi + 1e-6 * um) : rmax[i];
+    }
     Geometry geo;
     double m = 0.0;
     for (int i = 0; i < 3; ++i) {
-        geo.lo[i] = static_cast<double>(rmin[i]);
-        geo.ext[i] = static_cast<double>(rmax[i]) - static_cast<double>(rmin[i]);
+        geo.lo[i] = static_cast<double>(out.rmin[i]);
+        geo.ext[i] = static_cast<double>(out.rmax[i]) - static_cast<double>(out.rmin[i]);
         m = std::max(m, geo.ext[i]);
     }
     geo.margin = 1e-6 * m;

@@ -14,6 +14,7 @@ struct BuiltOctree {
     std::vector<HostNode> nodes;     // nodes[0] = root
     std::vector<float> prim_sp;      // 4 floats per leaf reference
     std::vector<uint32_t> prim_idx;  // sphere index per leaf reference
+    float rmin[3], rmax[3];          // effective root box (see build_octree)
     bool root_is_leaf = false;
     uint32_t n_leaves = 0;
     uint32_t depth_reached = 0;
@@ -22,9 +23,10 @@ struct BuiltOctree {
 // SURVEY.md 8d D2 generator (splitmix64 -> PCG32).
 void generate_spheres(uint32_t n, uint32_t seed, float* spheres, uint32_t* albedo);
 
-// Octree over [rmin, rmax]: split a cell while it holds more than leaf_cap
-// spheres and depth < max_depth; sphere/cell overlap is the conservative
-// double-precision test of DESIGN.md "Octree build".
+// Octree over [rmin, rmax] grown (only where needed, by a 1e-6*extent margin)
+// to enclose every sphere's AABB: split a cell while it holds more than
+// leaf_cap spheres and depth < max_depth; sphere/cell overlap is the
+// conservative double-precision test of DESIGN.md "Octree build".
 void build_octree(const float* spheres, uint32_t n, const float rmin[3], const float rmax[3],
                   uint32_t max_depth, uint32_t leaf_cap, BuiltOctree& out);
 

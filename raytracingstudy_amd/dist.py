@@ -1,0 +1,67 @@
+"""Multi-GPU frame sharding: one process per GPU, tiles + gather to rank 0.
+
+SURVEY.md 8e: 64x64 tiles dealt round-robin over R ranks; each rank renders
+its tiles into a packed slab (``rt_render_tiles``); rank 0 gathers the
+equal-size slabs over RCCL (``torch.distributed.gather``: on the nccl backend
+each peer's slab travels over its own xGMI link to rank 0) and scatters them
+into the frame (``rt_unpack_tiles``).  The scene is replicated: every rank
+builds it from the same seed, so there is no broadcast.
+
+The class is backend-agnostic: the GPU path passes CUDA tensors and the
+renderer's unpack kernel; the CPU tests use gloo with host tensors.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional
+
+import numpy as np
+
+from . import tiles as T
+
+__all__ = ["TileSharder"]
+
+
+class TileSharder:
+    def __init__(self, width: int, height: int, rank: int, world: int, tile_size: int = 64,
+                 channels: int = 4):
+        self.width, self.height = int(width), int(height)
+        self.rank, self.world = int(rank), int(world)
+        self.ts = int(tile_size)
+        self.channels = channels
+        self.all_ids: List[np.ndarray] = [T.tiles_for_rank(width, height, k, world, tile_size)
+                                          for k in range(world)]
+        self.ids = self.all_ids[self.rank]
+        self.slab_tiles = T.slab_tiles(width, height, world, tile_size)
+        self.slab_elems = self.slab_tiles * self.ts * self.ts * channels
+
+    def new_slab(self, torch_mod, device=None, dtype=None):
+        """Zeroed packed slab for this rank (uint8 RGBA by default)."""
+        dtype = dtype if dtype is not None else torch_mod.uint8
+        return torch_mod.zeros(self.slab_elems, dtype=dtype, device=device)
+
+    def gather(self, slab, group=None):
+        """Equal-size gather of every rank's slab to rank 0; returns the list on rank 0."""
+        import torch
+        import torch.distributed as dist
+        out = [torch.empty_like(slab) for _ in range(self.world)] if self.rank == 0 else None
+        if self.world == 1:
+            return [slab]
+        dist.gather(slab, out, dst=0, group=group)
+        return out
+
+    def unpack(self, gathered, unpack_fn: Callable[[object, np.ndarray], None]) -> None:
+        """Rank 0: call unpack_fn(slab_k, tile_ids_k) for every rank's slab."""
+        if self.rank != 0:
+            return
+        for k in range(self.world):
+            unpack_fn(gathered[k], self.all_ids[k])
+
+    def unpack_host(self, gathered, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """CPU restatement of the unpack (tests / host-only ranks)."""
+        if out is None:
+            out = np.zeros((self.height, self.width, self.channels), np.uint8)
+        for k in range(self.world):
+            ids = self.all_ids[k]
+            packed = np.asarray(gathered[k].cpu().numpy()).reshape(-1, self.ts, self.ts, self.channels)
+            T.unpack_host(packed[:len(ids)], ids, self.width, self.height, self.ts, out)
+        return out

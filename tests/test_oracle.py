@@ -1,0 +1,183 @@
+"""CPU tests of the oracle: pinned to the reference's known answers, then to
+its own golden fixtures and to brute-force checks of the octree walk."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+SEED = 0x2545F491
+
+
+def _pose(x, y, z):
+    p = np.zeros((4, 4), np.float32)
+    p[0, 0], p[1, 1], p[2, 2], p[3, 3] = 1, -1, -1, 1
+    p[3, :3] = (x, y, z)
+    return p
+
+
+def test_c1_known_answers(oracle):
+    """the reference-compat C1 image."""
+    ka = json.load(open(os.path.join(GOLD, "c1_known_answers.json")))
+    K = oracle.resize_intrinsic(ka["width"], ka["height"])
+    assert abs(K[0, 0] - ka["focal"]) < 1e-4 and K[0, 2] == ka["cx"] and K[1, 2] == ka["cy"]
+    pose = np.array(ka["pose_colmajor"], np.float32).reshape(4, 4)
+    img = oracle.render_compat(ka["width"], ka["height"], pose, K)
+    white = (img == 255).all(-1)
+    assert int(white.sum()) == ka["white_pixels"]
+    ys, xs = np.nonzero(white)
+    assert [xs.min(), ys.min(), xs.max(), ys.max()] == ka["white_bbox_xyxy"]
+    for x, y, rgba in ka["pixels_xy_rgba"]:
+        assert list(img[y, x]) == rgba
+    assert int(img.sum(dtype=np.int64)) == ka["byte_sum"]
+    assert np.array_equal(img, np.load(os.path.join(GOLD, "c1_compat.npy")))
+
+
+def test_behind_camera_quirk(oracle):
+    """hit_sphere has no t >= 0 test (src/renderer.cu:52): a box behind the ray hits."""
+    ka = json.load(open(os.path.join(GOLD, "c1_known_answers.json")))["behind_camera_quirk"]
+    o = np.array(ka["origin"], np.float32)
+    d = np.array(ka["dir"], np.float32)
+    lib = oracle.load()
+    assert bool(lib.orc_hit_root_box(oracle._p(o), oracle._p(d))) is ka["hit"]
+
+
+def test_compat_1080p_hash(oracle):
+    K = oracle.resize_intrinsic(1920, 1080)
+    img = oracle.render_compat(1920, 1080, _pose(0, 0, 3), K)
+    want = open(os.path.join(GOLD, "compat_1080p.sha256")).read().strip()
+    assert hashlib.sha256(img.tobytes()).hexdigest() == want
+
+
+def test_get_ray_is_unit_and_axis_exact(oracle):
+    K = oracle.resize_intrinsic(256, 256)
+    d = oracle.get_ray(_pose(0, 0, 3), K, 128.0, 128.0)
+    assert list(d) == [0.0, 0.0, -1.0]
+    d = oracle.get_ray(_pose(0, 0, 3), K, 3.0, 250.0)
+    assert abs(float(np.dot(d, d)) - 1.0) < 1e-6
+
+
+@pytest.mark.parametrize("name", ["scene_small", "scene_depth12"])
+def test_scene_goldens(oracle, name):
+    z = np.load(os.path.join(GOLD, name + ".npz"))
+    n, w, h, spp, depth, seed = (int(v) for v in z["params"])
+    sp, al = oracle.generate_spheres(n, SEED)
+    assert hashlib.sha256(sp.tobytes()).digest() == z["spheres_sha256"].tobytes()
+    assert hashlib.sha256(al.tobytes()).digest() == z["albedo_sha256"].tobytes()
+    sc = oracle.Scene(sp, al, max_depth=depth)
+    rgba8, rad, cnt = sc.render(w, h, _pose(0.64, 0.64, 2.2), oracle.resize_intrinsic(w, h),
+                                spp=spp, seed=seed)
+    assert np.array_equal(rgba8, z["rgba8"])
+    assert np.array_equal(rad, z["radiance"])
+    assert np.array_equal(cnt, z["counters"])
+
+
+def test_render_is_deterministic_across_threads(oracle):
+    sp, al = oracle.generate_spheres(2000, SEED)
+    sc = oracle.Scene(sp, al)
+    K = oracle.resize_intrinsic(64, 48)
+    a = sc.render(64, 48, _pose(0.64, 0.64, 2.2), K, spp=3, n_threads=1)
+    b = sc.render(64, 48, _pose(0.64, 0.64, 2.2), K, spp=3, n_threads=4)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+def test_row_subsample_matches_full(oracle):
+    sp, al = oracle.generate_spheres(1000, SEED)
+    sc = oracle.Scene(sp, al)
+    K = oracle.resize_intrinsic(80, 64)
+    full, fr, _ = sc.render(80, 64, _pose(0.64, 0.64, 2.2), K, spp=2)
+    sub, sr, _ = sc.render(80, 64, _pose(0.64, 0.64, 2.2), K, spp=2, row_step=8, row_phase=3)
+    rows = np.arange(3, 64, 8)
+    assert np.array_equal(full[rows], sub[rows])
+    mask = np.ones(64, bool)
+    mask[rows] = False
+    assert not sub[mask].any()
+
+
+def _rays(rng, n, inside_frac=0.5, axis_frac=0.2):
+    for k in range(n):
+        if rng.random() < inside_frac:
+            o = rng.uniform(0, 1.28, 3)
+        else:
+            o = np.array([0.64, 0.64, 2.2]) + rng.normal(0, 0.1, 3)
+        d = rng.normal(0, 1, 3)
+        if rng.random() < axis_frac:
+            d[rng.integers(3)] = 0.0
+            if rng.random() < 0.5:
+                d[rng.integers(3)] = -0.0
+        d /= np.linalg.norm(d)
+        yield o.astype(np.float32), d.astype(np.float32)
+
+
+@pytest.mark.parametrize("n,depth,leaf", [(1000, 7, 8), (30000, 7, 8), (5000, 12, 2), (200, 3, 1)])
+def test_walk_matches_brute_force(oracle, n, depth, leaf):
+    """The octree walk is conservative: nearest hit (t, index) and any-hit equal
+    an exhaustive test of every sphere, including axis-parallel (+-0) rays."""
+    sp, al = oracle.generate_spheres(n, SEED)
+    sc = oracle.Scene(sp, al, max_depth=depth, leaf_capacity=leaf)
+    rng = np.random.default_rng(n + depth)
+    for o, d in _rays(rng, 1500):
+        for anyh in (False, True):
+            h1, t1, i1, _ = sc.trace(o, d, any_hit=anyh)
+            h2, t2, i2, _ = sc.trace(o, d, any_hit=anyh, brute=True)
+            assert h1 == h2
+            if h1 and not anyh:
+                assert (t1, i1) == (t2, i2)
+
+
+def test_walk_tmax_and_grid_aligned_rays(oracle):
+    sp = np.array([[0.32, 0.32, 0.32, 0.05], [0.96, 0.32, 0.32, 0.05]], np.float32)
+    sc = oracle.Scene(sp, None, max_depth=7, leaf_capacity=1)
+    # ray exactly along a cell boundary plane (x = 0.32 is a grid plane at depth 2)
+    h, t, i, _ = sc.trace([0.32, 0.32, 2.0], [0.0, 0.0, -1.0])
+    assert h and i == 0 and abs(t - (2.0 - 0.37)) < 1e-5
+    # tmax before the sphere: no hit
+    h, _, _, _ = sc.trace([0.32, 0.32, 2.0], [0.0, 0.0, -1.0], tmax=1.0)
+    assert not h
+    # ray along x through both spheres: nearest first, from either direction
+    h, t, i, _ = sc.trace([-1.0, 0.32, 0.32], [1.0, 0.0, 0.0])
+    assert h and i == 0
+    h, t, i, _ = sc.trace([2.0, 0.32, 0.32], [-1.0, 0.0, 0.0])
+    assert h and i == 1
+
+
+def test_empty_and_outside(oracle):
+    sc = oracle.Scene(np.zeros((0, 4), np.float32), None)
+    assert sc.info()["n_nodes"] == 1
+    h, _, _, _ = sc.trace([0.5, 0.5, 3.0], [0, 0, -1])
+    assert not h
+    sp, al = oracle.generate_spheres(100, SEED)
+    sc = oracle.Scene(sp, al)
+    h, _, _, c = sc.trace([5.0, 5.0, 5.0], [1.0, 0.0, 0.0])  # pointing away from the box
+    assert not h and c[2] == 0 and c[3] == 0
+
+
+def test_octree_build_invariants(oracle):
+    sp, al = oracle.generate_spheres(50000, SEED)
+    for depth in (7, 12):
+        info = oracle.Scene(sp, al, max_depth=depth).info()
+        assert info["depth_reached"] <= depth
+        assert info["n_prim_refs"] >= 50000  # every sphere is in >= 1 leaf
+        assert info["n_leaves"] < info["n_nodes"]
+
+
+def test_depth_for_resolution(oracle):
+    lib = oracle.load()
+    mn = np.zeros(3, np.float32)
+    mx = np.full(3, 1.28, np.float32)
+    # reference: resolution 0.01 over 1.28 -> 128 cells -> depth 7 (src/renderer.cu:134-136)
+    assert lib.orc_depth_for_resolution(oracle._p(mn), oracle._p(mx), 0.01) == 7
+    assert lib.orc_depth_for_resolution(oracle._p(mn), oracle._p(mx), 1.28 / 4096) == 12
+
+
+def test_sample_hash_distribution(oracle):
+    lib = oracle.load()
+    v = np.array([lib.orc_sample_hash(SEED, pid, s, d) for pid in range(64) for s in range(16)
+                  for d in range(2)], np.uint64)
+    u = (v >> 8).astype(np.float64) / 2 ** 24
+    assert len(np.unique(v)) == len(v)
+    assert abs(u.mean() - 0.5) < 0.03
