@@ -1,0 +1,94 @@
+// rt_renderer.hpp — header-only C++ host surface with the reference's
+// KernelRenderer method names (include/renderer.cuh:25-50), forwarding to the
+// C-ABI in rt.h.  A maintainer swaps `#include "renderer.cuh"` for this header
+// in Displayer (src/window/displayer.cpp, include/window/displayer.h) and
+// passes glm::value_ptr(...) where the reference passed glm matrices by value.
+//
+// Differences from the reference, all additive:
+//   * every method reports failure (throws rtamd::Error with the library's
+//     message) instead of returning void silently (src/renderer.cu:143-153);
+//   * render() takes the device pointer the GL PBO maps to (the caller keeps
+//     hipGraphicsMapResources / hipGraphicsUnmapResources, exactly where the
+//     reference calls cudaGraphicsMapResources at src/renderer.cu:145-151),
+//     or nullptr for the renderer's own framebuffer;
+//   * setOctree (declared but never defined in the reference,
+//     include/renderer.cuh:35) is implemented, and setScene adds spheres.
+#pragma once
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "rt.h"
+
+namespace rtamd {
+
+class Error : public std::runtime_error {
+public:
+    Error(int code, const std::string& msg) : std::runtime_error(msg), code(code) {}
+    int code;
+};
+
+inline void check(int code, const rt_renderer* r = nullptr) {
+    if (code != RT_OK) throw Error(code, rt_last_error(r));
+}
+
+class KernelRenderer {
+public:
+    // Reference: KernelRenderer(cudaGraphicsResource_t, int width, int height)
+    // (src/renderer.cu:124-141).  The graphics resource stays with the caller.
+    KernelRenderer(int width, int height, uint32_t mode = RT_MODE_COMPAT, uint32_t spp = 1,
+                   int device = -1) {
+        rt_config cfg;
+        rt_config_default(&cfg);
+        cfg.width = static_cast<uint32_t>(width);
+        cfg.height = static_cast<uint32_t>(height);
+        cfg.mode = mode;
+        cfg.spp = spp;
+        cfg.device = device;
+        check(rt_create(&cfg, &r_));
+    }
+    explicit KernelRenderer(const rt_config& cfg) { check(rt_create(&cfg, &r_)); }
+    ~KernelRenderer() { rt_destroy(r_); }
+    KernelRenderer(const KernelRenderer&) = delete;
+    KernelRenderer& operator=(const KernelRenderer&) = delete;
+
+    // render() (src/renderer.cu:143-153): dev_rgba8 = mapped PBO pointer.
+    void render(void* dev_rgba8 = nullptr, void* stream = nullptr, rt_stats* stats = nullptr) {
+        check(rt_render(r_, dev_rgba8, stream, stats), r_);
+    }
+    // resize(int, int) (src/renderer.cu:155-187)
+    void resize(int width, int height) {
+        check(rt_resize(r_, static_cast<uint32_t>(width), static_cast<uint32_t>(height)), r_);
+    }
+    // setPosition(glm::mat4) (src/renderer.cu:111-113): pass glm::value_ptr(pose)
+    void setPosition(const float* pose_colmajor16) { check(rt_set_pose(r_, pose_colmajor16), r_); }
+    // setIntrinsic(glm::mat3) (src/renderer.cu:115-117): pass glm::value_ptr(K)
+    void setIntrinsic(const float* K_colmajor9) { check(rt_set_intrinsic(r_, K_colmajor9), r_); }
+    // setOctree(glm::vec3 min, glm::vec3 max, float resolution) (include/renderer.cuh:35)
+    void setOctree(const float* min3, const float* max3, float resolution) {
+        check(rt_set_octree(r_, min3, max3, resolution), r_);
+    }
+    // new: spheres (cx, cy, cz, r) x n, optional RGBA8 albedo
+    void setScene(const std::vector<float>& spheres, const std::vector<uint32_t>& albedo = {},
+                  const rt_octree_params* oct = nullptr) {
+        const uint32_t n = static_cast<uint32_t>(spheres.size() / 4);
+        check(rt_set_scene(r_, spheres.data(), albedo.empty() ? nullptr : albedo.data(), n, oct),
+              r_);
+    }
+    rt_scene_info sceneInfo() const {
+        rt_scene_info i;
+        check(rt_get_scene_info(r_, &i), r_);
+        return i;
+    }
+    void readback(uint8_t* host_rgba8, float* host_rgba32f = nullptr) {
+        check(rt_readback(r_, host_rgba8, host_rgba32f), r_);
+    }
+    void synchronize() { check(rt_synchronize(r_), r_); }
+    rt_renderer* handle() { return r_; }
+
+private:
+    rt_renderer* r_ = nullptr;
+};
+
+}  // namespace rtamd

@@ -150,3 +150,94 @@ def test_tiles_match_frame(gpu):
         r.unpack_tiles(packed.data_ptr(), ids, ts, img.data_ptr())
         r.synchronize()
         assert np.array_equal(img.cpu().numpy().reshape(h, w, 4), full)
+
+
+@pytest.mark.parametrize("case", ["inside", "yawed", "grazing_axis", "far"])
+def test_scene_camera_cases(gpu, oracle, case):
+    """Camera inside the octree, off-axis poses, axis-aligned rays, distant camera."""
+    pose = {"inside": translation_pose(0.64, 0.64, 0.64),
+            "yawed": display_pose((1.9, 1.4, 1.9), 40.0, -25.0),
+            "grazing_axis": translation_pose(0.32, 0.32, 2.0),
+            "far": translation_pose(0.64, 0.64, 40.0)}[case]
+    img, rad, st, info, ref8, ref32, cnt, _ = _scene_pair(oracle, 5000, 160, 96, 2, pose=pose)
+    assert np.array_equal(img, ref8)
+    assert np.array_equal(rad, ref32)
+    assert (st.shadow_rays, st.nodes_visited, st.prims_tested) == tuple(int(c) for c in cnt[1:])
+
+
+def test_scene_no_shadows_no_jitter(gpu, oracle):
+    img, rad, st, _, ref8, ref32, cnt, _ = _scene_pair(oracle, 3000, 120, 80, 3, shadows=False,
+                                                        jitter=False)
+    assert st.shadow_rays == 0 == cnt[1]
+    assert np.array_equal(img, ref8) and np.array_equal(rad, ref32)
+
+
+def test_scene_custom_root_and_resolution(gpu, oracle):
+    """setOctree(min, max, resolution) (include/renderer.cuh:35) with a non-cubic box."""
+    sp, al = rt.generate_spheres(4000, rt.SEED)
+    sp = sp.copy()
+    sp[:, 0] = sp[:, 0] * 2.0 - 0.5
+    w, h = 128, 80
+    with rt.KernelRenderer(w, h, mode="scene", spp=1, radiance=True) as r:
+        r.resize(w, h)
+        r.setPosition(display_pose((0.8, 0.6, 3.0), 0.0, -5.0))
+        r.set_scene(sp, al)
+        r.setOctree((-0.5, 0.0, 0.0), (2.06, 1.28, 1.28), 0.02)
+        info = r.scene_info()
+        st = r.render(stats=True)
+        img, rad = r.readback(), r.readback_radiance()
+        pose, K = r.camera()
+    mn = np.array([-0.5, 0, 0], np.float32)
+    mx = np.array([2.06, 1.28, 1.28], np.float32)
+    depth = oracle.load().orc_depth_for_resolution(oracle._p(mn), oracle._p(mx), 0.02)
+    assert info["max_depth"] == depth
+    sc = oracle.Scene(sp, al, root_min=(-0.5, 0, 0), root_max=(2.06, 1.28, 1.28), max_depth=depth)
+    ref8, ref32, cnt = sc.render(w, h, pose, K, spp=1)
+    assert np.array_equal(img, ref8) and np.array_equal(rad, ref32)
+    assert st.nodes_visited == cnt[2] and st.prims_tested == cnt[3]
+
+
+def test_external_buffer_and_stream(gpu):
+    """render(dev_ptr, stream): the GL-PBO-style path (src/renderer.cu:145-151)."""
+    import torch
+    w, h = 200, 120
+    sp, al = rt.generate_spheres(2000, rt.SEED)
+    with rt.KernelRenderer(w, h, mode="scene", spp=2) as r:
+        r.resize(w, h)
+        r.setPosition(scene_pose())
+        r.set_scene(sp, al)
+        r.render()
+        internal = r.readback()
+        s = torch.cuda.Stream()
+        buf = torch.zeros(w * h * 4, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        r.render(buf.data_ptr(), s.cuda_stream)
+        s.synchronize()
+        assert np.array_equal(buf.cpu().numpy().reshape(h, w, 4), internal)
+
+
+def test_resize_then_render(gpu, oracle):
+    sp, al = rt.generate_spheres(1000, rt.SEED)
+    with rt.KernelRenderer(64, 64, mode="scene", spp=1) as r:
+        r.setPosition(scene_pose())
+        r.set_scene(sp, al)
+        for (w, h) in [(64, 64), (333, 111), (17, 250)]:
+            r.resize(w, h)
+            r.render()
+            img = r.readback()
+            _, K = r.camera()
+            ref, _, _ = oracle.Scene(sp, al).render(w, h, scene_pose(), K, spp=1, radiance=False)
+            assert np.array_equal(img, ref), (w, h)
+
+
+def test_errors_are_loud(gpu):
+    with rt.KernelRenderer(32, 32, mode="scene") as r:
+        with pytest.raises(rt._lib.RtError) as e:
+            r.render()  # no scene yet
+        assert e.value.code == rt._lib.RT_E_NOSCENE
+        with pytest.raises(rt._lib.RtError):
+            r.set_scene(np.array([[0, 0, 0, -1]], np.float32))
+        with pytest.raises(rt._lib.RtError):
+            r.render_tiles([0], 48, 0)  # tile size not a multiple of 64
+        with pytest.raises(rt._lib.RtError):
+            r.readback_radiance()  # no RT_FLAG_RADIANCE

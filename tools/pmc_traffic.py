@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run into one JSON object (per-launch figures).
+
+    python tools/pmc_traffic.py gpurun_out/prof_<tag> <config> > pmc_summary.json
+
+HBM traffic follows MI355X_MICROARCH.md "HBM": FETCH_SIZE / WRITE_SIZE are in
+KiB and come from separate --pmc passes; on gfx950 FETCH_SIZE reports half the
+bytes of wide coalesced reads, so the corrected read bytes are 2 x FETCH_SIZE
+(the raw sum is reported beside it; the guide notes other access widths are
+uncalibrated).  Counters are averaged over every dispatch of the scene kernel.
+"""
+from __future__ import annotations
+
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def _rows(pattern):
+    out = []
+    for path in sorted(glob.glob(pattern, recursive=True)):
+        with open(path, newline="") as f:
+            out.extend(csv.DictReader(f))
+    return out
+
+
+def counters(d, kernel_sub="scene_kernel"):
+    per = defaultdict(lambda: defaultdict(float))
+    for r in _rows(os.path.join(d, "**", "*counter_collection.csv")):
+        if kernel_sub not in r.get("Kernel_Name", ""):
+            continue
+        per[r["Counter_Name"]][r.get("Dispatch_Id", r.get("Correlation_Id"))] += float(r["Counter_Value"])
+    return {k: (sum(v.values()) / len(v), len(v)) for k, v in per.items() if v}
+
+
+def kernel_stats(d):
+    out = {}
+    for r in _rows(os.path.join(d, "**", "*kernel_stats.csv")):
+        out[r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                          "total_ns": float(r["TotalDurationNs"]), "pct": float(r["Percentage"])}
+    return out
+
+
+def trace_durations(d, kernel_sub="scene_kernel"):
+    ds = []
+    for r in _rows(os.path.join(d, "**", "*kernel_trace.csv")):
+        if kernel_sub in r.get("Kernel_Name", ""):
+            ds.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    return ds
+
+
+def main():
+    root, cfg = sys.argv[1], sys.argv[2]
+    res = {"config": cfg, "n_gpus": 1}
+    ks = kernel_stats(os.path.join(root, "trace"))
+    res["kernel_stats"] = ks
+    durs = trace_durations(os.path.join(root, "trace"))
+    if durs:
+        res["scene_kernel_dispatches"] = len(durs)
+        res["scene_kernel_avg_ns"] = sum(durs) / len(durs)
+    f = counters(os.path.join(root, "fetch")).get("FETCH_SIZE")
+    w = counters(os.path.join(root, "write")).get("WRITE_SIZE")
+    if f and w:
+        res["fetch_size_kib"] = f[0]
+        res["write_size_kib"] = w[0]
+        res["hbm_bytes_raw"] = (f[0] + w[0]) * 1024.0
+        res["hbm_bytes_per_launch"] = (2.0 * f[0] + w[0]) * 1024.0
+        res["correction"] = "gfx950: read bytes = 2 x FETCH_SIZE (MI355X_MICROARCH.md HBM); KiB -> B"
+    sq = counters(os.path.join(root, "sq"))
+    if sq:
+        res["sq"] = {k: v[0] for k, v in sq.items()}
+        waves = sq.get("SQ_WAVES", (0, 0))[0]
+        cyc = sq.get("SQ_WAVE_CYCLES", (0, 0))[0]
+        act = sq.get("SQ_ACTIVE_INST_VALU", (0, 0))[0]
+        gui = sq.get("GRBM_GUI_ACTIVE", (0, 0))[0]
+        if cyc:
+            res["valu_active_frac_of_wave_cycles"] = act / cyc
+        if gui and durs:
+            res["effective_clock_ghz"] = gui / 8.0 / (sum(durs) / len(durs))
+        if waves:
+            res["valu_insts_per_wave"] = sq.get("SQ_INSTS_VALU", (0, 0))[0] / waves
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
