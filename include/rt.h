@@ -76,7 +76,10 @@ enum {
     RT_FLAG_JITTER = 1u << 0,      /* per-sample sub-pixel jitter (default: on iff spp > 1) */
     RT_FLAG_NO_JITTER = 1u << 1,   /* force jitter off */
     RT_FLAG_RADIANCE = 1u << 2,    /* also keep the float4 mean radiance buffer */
-    RT_FLAG_NO_SHADOWS = 1u << 3   /* skip shadow rays (Lambert without visibility) */
+    RT_FLAG_NO_SHADOWS = 1u << 3,  /* skip shadow rays (Lambert without visibility) */
+    /* bits 16..19: scene-kernel variant for A/B runs (0 = default = 1, one ray
+     * per lane; 2 = 64-ray wave packets); images are identical */
+    RT_FLAG_VARIANT_SHIFT = 16
 };
 
 typedef struct rt_config {

@@ -28,6 +28,9 @@ RT_FLAG_JITTER = 1 << 0
 RT_FLAG_NO_JITTER = 1 << 1
 RT_FLAG_RADIANCE = 1 << 2
 RT_FLAG_NO_SHADOWS = 1 << 3
+RT_FLAG_VARIANT_SHIFT = 16
+VARIANT_LANE = 1    # one ray per lane
+VARIANT_PACKET = 2  # 64-ray wave packets (default)
 
 _f3 = ctypes.c_float * 3
 

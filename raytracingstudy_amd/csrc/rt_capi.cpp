@@ -24,7 +24,6 @@ hipError_t launch_scene(const FrameArgs& a, hipStream_t st);
 hipError_t launch_unpack(const uint32_t* packed, const uint32_t* tiles, uint32_t n_tiles,
                          uint32_t ts, uint32_t tiles_x, uint32_t W, uint32_t H, uint32_t* img,
                          hipStream_t st);
-size_t scene_lds_bytes(uint32_t max_depth);
 }  // namespace rtamd
 
 using namespace rtamd;
@@ -138,6 +137,8 @@ void fill_frame_args(rt_renderer* r, FrameArgs& a) {
     a.ambient = r->cfg.ambient;
     a.inv_spp = 1.0f / static_cast<float>(a.spp);
     a.counters = r->counters.p;
+    const uint32_t v = (r->cfg.flags >> RT_FLAG_VARIANT_SHIFT) & 0xFu;
+    a.variant = v ? v : kVariantDefault;
 }
 
 int upload_scene(rt_renderer* r) {

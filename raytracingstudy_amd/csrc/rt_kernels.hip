@@ -11,6 +11,8 @@
 // source order with IEEE division/sqrt, exactly like oracle/oracle.c.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "rt_params.h"
 
 namespace rtamd {
@@ -250,68 +252,219 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
     return false;
 }
 
+// ---------------------------------------------------------------------------
+// Packet variant: the wave walks the octree as ONE 64-ray packet.
+//
+// An 8x8 pixel block's jittered primary rays are coherent, and all shadow
+// rays share the light direction, so the union of the cells the 64 rays cross
+// is close to one ray's.  The wave therefore keeps ONE traversal stack (in
+// LDS, per wave) of (node record, cell, 64-bit lane mask) entries:
+//   * children of an internal node are culled per lane with the same grid
+//     plane formula as walk<> (entry/exit of every child from 9 planes) and
+//     pushed far-to-near (front-to-back for the majority mirror octant) with
+//     their __ballot lane mask; empty masks are never pushed;
+//   * a popped entry re-checks its lanes against best_t (nearest) / done
+//     (any-hit); a zero mask skips the node for the whole wave;
+//   * node records and sphere records are read at wave-uniform addresses
+//     (scalar loads, broadcast) and each sphere is tested by all active lanes.
+// Per-lane results are the nearest (t, index) over every sphere whose cells
+// the ray crosses — the same definition the oracle's walk computes (order-
+// independent: ties go to the smaller index), so images are bit-identical.
+// Counters: nodes = lane-node visits, prims = lane-sphere tests (work done).
+// ---------------------------------------------------------------------------
+
+struct PStackEntry {
+    uint32_t rx, ry;   // node record
+    uint32_t c01;      // c0 | c1 << 16   (REAL grid coordinates at `depth`)
+    uint32_t c2dl;     // c2 | depth << 16 | leaf << 24
+    uint32_t mlo, mhi; // lane mask
+    uint32_t pad0, pad1;
+};
+
+__device__ __forceinline__ uint32_t ufirst(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+template <bool kAnyHit>
+__device__ __forceinline__ bool walk_packet(const SceneArgs& S, bool want, float o0, float o1,
+                                            float o2, float d0, float d1, float d2, float tmin,
+                                            float& tout, uint32_t& iout, uint32_t& n_nodes,
+                                            uint32_t& n_prims, PStackEntry* __restrict__ stk) {
+    const uint32_t G = 1u << S.max_depth;
+    const float o[3] = {o0, o1, o2};
+    const float d[3] = {d0, d1, d2};
+    float og[3], inv[3];
+    bool mir[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float g = (o[i] - S.rmin[i]) * S.scale[i];
+        mir[i] = d[i] < 0.0f;
+        float a = fabsf(d[i]);
+        if (a < 1e-20f) a = 1e-20f;
+        og[i] = mir[i] ? S.G - g : g;
+        inv[i] = 1.0f / (a * S.scale[i]);
+    }
+    // t of the plane at REAL grid coordinate k, in this lane's mirrored frame
+    auto P = [&](int i, uint32_t k) {
+        const uint32_t km = mir[i] ? G - k : k;
+        return (static_cast<float>(km) - og[i]) * inv[i];
+    };
+    auto plane_m = [&](int i, uint32_t km) { return (static_cast<float>(km) - og[i]) * inv[i]; };
+    float t0 = plane_m(0, 0), t1 = plane_m(0, G);
+#pragma unroll
+    for (int i = 1; i < 3; ++i) {
+        const float a0 = plane_m(i, 0), a1 = plane_m(i, G);
+        if (a0 > t0) t0 = a0;
+        if (a1 < t1) t1 = a1;
+    }
+    if (t0 < tmin) t0 = tmin;
+    bool on = want && (t0 < t1);
+    float best_t = INFINITY;
+    uint32_t best = kNoHit;
+    bool done = false;
+    const uint64_t m0 = __ballot(on);
+    if (m0 == 0) return false;
+    n_nodes += on ? 1u : 0u;
+
+    // majority mirror octant -> front-to-back child order for the packet
+    const uint32_t pop = __popcll(m0);
+    uint32_t rm = 0;
+    if (2u * __popcll(__ballot(on && mir[0])) > pop) rm |= 1u;
+    if (2u * __popcll(__ballot(on && mir[1])) > pop) rm |= 2u;
+    if (2u * __popcll(__ballot(on && mir[2])) > pop) rm |= 4u;
+
+    const float4* __restrict__ prim_sp = S.prim_sp;
+    const uint32_t* __restrict__ prim_idx = S.prim_idx;
+    const uint2* __restrict__ nodes = S.nodes;
+    const uint32_t lane = __lane_id();
+
+    auto do_leaf = [&](uint32_t off, uint32_t cnt, bool lane_on) {
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const float4 sp = prim_sp[off + j];
+            const uint32_t idx = kAnyHit ? 0u : prim_idx[off + j];
+            if (lane_on) {
+                n_prims += 1;
+                float th;
+                if (isect(o0, o1, o2, d0, d1, d2, sp, tmin, INFINITY, th)) {
+                    if (kAnyHit) {
+                        done = true;
+                        lane_on = false;
+                        tout = th;
+                    } else if (th < best_t || (th == best_t && idx < best)) {
+                        best_t = th;
+                        best = idx;
+                    }
+                }
+            }
+            if (kAnyHit && __ballot(lane_on) == 0) break;
+        }
+    };
+
+    int top = 0;
+    auto expand = [&](uint32_t depth, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t rx,
+                      uint32_t ry, bool lane_on) {
+        const uint32_t h = G >> (depth + 1);
+        const uint32_t cc[3] = {c0, c1, c2};
+        float E0[3], X0[3], E1[3], X1[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const uint32_t lo = cc[i] * 2u * h;
+            const float pl = P(i, lo), pm = P(i, lo + h), ph = P(i, lo + 2u * h);
+            E0[i] = mir[i] ? pm : pl;
+            X0[i] = mir[i] ? pl : pm;
+            E1[i] = mir[i] ? ph : pm;
+            X1[i] = mir[i] ? pm : ph;
+        }
+        const uint32_t valid = ry & 0xFFu, leafm = (ry >> 8) & 0xFFu;
+        // push far -> near: order {0,1,2,4,3,5,6,7} ^ rm is front-to-back
+        const uint32_t ord[8] = {7, 6, 5, 3, 4, 2, 1, 0};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t ch = ord[k] ^ rm;
+            if (!((valid >> ch) & 1u)) continue;
+            const uint32_t b0 = ch & 1u, b1 = (ch >> 1) & 1u, b2 = ch >> 2;
+            float te = fmaxf(fmaxf(b0 ? E1[0] : E0[0], b1 ? E1[1] : E0[1]), b2 ? E1[2] : E0[2]);
+            float tx = fminf(fminf(b0 ? X1[0] : X0[0], b1 ? X1[1] : X0[1]), b2 ? X1[2] : X0[2]);
+            te = te < tmin ? tmin : te;
+            tx = tx > t1 ? t1 : tx;
+            const bool ok = lane_on && te <= tx && (kAnyHit ? !done : te <= best_t);
+            const uint64_t mk = __ballot(ok);
+            if (mk == 0) continue;
+            const uint32_t slot = rx + __builtin_popcount(valid & ((1u << ch) - 1u));
+            const uint2 crec = nodes[slot];
+            if (lane == 0) {
+                PStackEntry e;
+                e.rx = crec.x;
+                e.ry = crec.y;
+                e.c01 = (2u * c0 + b0) | ((2u * c1 + b1) << 16);
+                e.c2dl = (2u * c2 + b2) | ((depth + 1u) << 16) | (((leafm >> ch) & 1u) << 24);
+                e.mlo = static_cast<uint32_t>(mk);
+                e.mhi = static_cast<uint32_t>(mk >> 32);
+                e.pad0 = e.pad1 = 0;
+                stk[top] = e;
+            }
+            ++top;
+        }
+    };
+
+    if (S.root_is_leaf) {
+        do_leaf(S.root.x, S.root.y, on);
+    } else {
+        expand(0, 0, 0, 0, S.root.x, S.root.y, on);
+        while (top > 0) {
+            --top;
+            const PStackEntry e = stk[top];
+            const uint32_t rx = ufirst(e.rx), ry = ufirst(e.ry);
+            const uint32_t c01 = ufirst(e.c01), c2dl = ufirst(e.c2dl);
+            const uint64_t mk = (static_cast<uint64_t>(ufirst(e.mhi)) << 32) | ufirst(e.mlo);
+            const uint32_t c0 = c01 & 0xFFFFu, c1 = c01 >> 16, c2 = c2dl & 0xFFFFu;
+            const uint32_t depth = (c2dl >> 16) & 0xFFu;
+            const bool leaf = (c2dl >> 24) & 1u;
+            bool lane_on = (mk >> lane) & 1u;
+            if (kAnyHit) {
+                lane_on = lane_on && !done;
+            } else if (lane_on) {
+                const uint32_t size = G >> depth;
+                const float e0 = P(0, mir[0] ? (c0 + 1u) * size : c0 * size);
+                const float e1 = P(1, mir[1] ? (c1 + 1u) * size : c1 * size);
+                const float e2 = P(2, mir[2] ? (c2 + 1u) * size : c2 * size);
+                float te = fmaxf(fmaxf(e0, e1), e2);
+                te = te < tmin ? tmin : te;
+                lane_on = te <= best_t;
+            }
+            if (__ballot(lane_on) == 0) continue;
+            n_nodes += lane_on ? 1u : 0u;
+            if (leaf)
+                do_leaf(rx, ry, lane_on);
+            else
+                expand(depth, c0, c1, c2, rx, ry, lane_on);
+            if (kAnyHit && __ballot(on && !done) == 0) break;
+        }
+    }
+    if (kAnyHit) return done;
+    if (best != kNoHit) {
+        tout = best_t;
+        iout = best;
+        return true;
+    }
+    return false;
+}
+
+// ---------------------------------------------------------------------------
+// Frame mapping, shading, ordered accumulation
+//
+// A wave owns `ppw` pixels x `spw` samples (host: spw = min(spp, 64),
+// ppw = pow2floor(64 / spw)); lane l works on pixel l / spw, sample
+// round * spw + l % spw.  At spp >= 64 all 64 lanes of a wave trace jittered
+// samples of ONE pixel: their primary rays stay within one pixel footprint and
+// their shadow rays start from nearly the same point with the same direction,
+// so the wave's lanes follow nearly the same octree path (little SIMD
+// divergence, and coherent packets).  The per-pixel mean keeps the oracle's
+// exact summation order: every lane parks its sample colour in LDS and the
+// pixel's leader lane adds them in sample order.
+// ---------------------------------------------------------------------------
+
 struct PixelOut {
     float r, g, b;
 };
-
-__device__ __forceinline__ PixelOut scene_pixel(const FrameArgs& a, uint32_t x, uint32_t y,
-                                                uint32_t& n_shadow, uint32_t& n_nodes,
-                                                uint32_t& n_prims, uint2* stk) {
-    const SceneArgs& S = a.sc;
-    const uint32_t pid = y * a.W + x;
-    const uint32_t hp = mix32(a.seedmix ^ pid);
-    const float miss_r = 200.0f / 255.0f;
-    float ar = 0.0f, ag = 0.0f, ab = 0.0f;
-    for (uint32_t s = 0; s < a.spp; ++s) {
-        float u = static_cast<float>(x), v = static_cast<float>(y);
-        if (a.jitter) {
-            u = u + u01(mix32(hp ^ (s << 1)));
-            v = v + u01(mix32(hp ^ ((s << 1) | 1u)));
-        }
-        float d0, d1, d2;
-        get_ray(a.cam, u, v, d0, d1, d2);
-        float t;
-        uint32_t idx;
-        float cr, cg, cb;
-        if (!walk<false>(S, a.cam.o[0], a.cam.o[1], a.cam.o[2], d0, d1, d2, 0.0f, INFINITY, t, idx,
-                         n_nodes, n_prims, stk)) {
-            cr = miss_r;
-            cg = sat(d1);
-            cb = sat(d2);
-        } else {
-            const float4 sp = S.spheres[idx];
-            const float p0 = a.cam.o[0] + t * d0;
-            const float p1 = a.cam.o[1] + t * d1;
-            const float p2 = a.cam.o[2] + t * d2;
-            const float ir = 1.0f / sp.w;
-            const float n0 = (p0 - sp.x) * ir;
-            const float n1 = (p1 - sp.y) * ir;
-            const float n2 = (p2 - sp.z) * ir;
-            const float ndl = n0 * a.L[0] + n1 * a.L[1] + n2 * a.L[2];
-            float lam = ndl > 0.0f ? ndl : 0.0f;
-            if (ndl > 0.0f && a.shadows) {
-                const float s0 = p0 + n0 * kShadowEps;
-                const float s1 = p1 + n1 * kShadowEps;
-                const float s2 = p2 + n2 * kShadowEps;
-                n_shadow += 1;
-                float ts;
-                uint32_t is;
-                if (walk<true>(S, s0, s1, s2, a.L[0], a.L[1], a.L[2], 0.0f, INFINITY, ts, is,
-                               n_nodes, n_prims, stk))
-                    lam = 0.0f;
-            }
-            const float f = a.ambient + (1.0f - a.ambient) * lam;
-            const uint32_t al = S.albedo[idx];
-            cr = static_cast<float>(al & 0xFFu) * (1.0f / 255.0f) * f;
-            cg = static_cast<float>((al >> 8) & 0xFFu) * (1.0f / 255.0f) * f;
-            cb = static_cast<float>((al >> 16) & 0xFFu) * (1.0f / 255.0f) * f;
-        }
-        ar += cr;
-        ag += cg;
-        ab += cb;
-    }
-    return {ar * a.inv_spp, ag * a.inv_spp, ab * a.inv_spp};
-}
 
 __device__ __forceinline__ uint32_t pack_rgba8(const PixelOut& p) {
     const uint32_t r = static_cast<uint32_t>(sat(p.r) * 255.0f);
@@ -340,42 +493,155 @@ __device__ __forceinline__ void flush_counters(const FrameArgs& a, uint32_t prim
     }
 }
 
-// 16x16 pixels per workgroup; wave w covers the 8x8 quadrant (w&1, w>>1),
-// lane -> (lane&7, lane>>3), so one wave's rays are a compact screen block.
-template <bool kTiles>
-__global__ void __launch_bounds__(kBlockThreads) scene_kernel(FrameArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint2 lds_stack[];
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t qx = (wave & 1u) * 8u + (lane & 7u);
-    const uint32_t qy = (wave >> 1) * 8u + (lane >> 3);
-    uint32_t x, y, k = 0, lx = 0, ly = 0;
-    if (kTiles) {
-        const uint32_t per = (a.tile_size / kTileSide) * (a.tile_size / kTileSide);
-        k = blockIdx.x / per;
-        const uint32_t sub = blockIdx.x % per;
-        lx = (sub % (a.tile_size / kTileSide)) * kTileSide + qx;
-        ly = (sub / (a.tile_size / kTileSide)) * kTileSide + qy;
-        const uint32_t tile = a.tiles[k];
-        x = (tile % a.tiles_x) * a.tile_size + lx;
-        y = (tile / a.tiles_x) * a.tile_size + ly;
-    } else {
-        x = blockIdx.x * kTileSide + qx;
-        y = blockIdx.y * kTileSide + qy;
+// One sample of pixel (x, y): primary walk, Lambert shade, shadow walk.
+// kVar selects the traversal; `valid` lanes trace, the others only take part
+// in the packet walks' wave-wide votes.
+template <uint32_t kVar>
+__device__ __forceinline__ PixelOut sample_color(const FrameArgs& a, uint32_t x, uint32_t y,
+                                                 uint32_t hp, uint32_t s, bool valid,
+                                                 uint32_t& n_shadow, uint32_t& n_nodes,
+                                                 uint32_t& n_prims, void* stk) {
+    const SceneArgs& S = a.sc;
+    float u = static_cast<float>(x), v = static_cast<float>(y);
+    if (a.jitter) {
+        u = u + u01(mix32(hp ^ (s << 1)));
+        v = v + u01(mix32(hp ^ ((s << 1) | 1u)));
     }
-    uint32_t n_shadow = 0, n_nodes = 0, n_prims = 0, n_primary = 0;
-    const bool inside = x < a.W && y < a.H;
-    if (inside) {
-        const PixelOut p = scene_pixel(a, x, y, n_shadow, n_nodes, n_prims, lds_stack + threadIdx.x);
-        n_primary = a.spp;
-        const uint32_t rgba = pack_rgba8(p);
-        if (kTiles) {
-            a.out8[(size_t)k * a.tile_size * a.tile_size + ly * a.tile_size + lx] = rgba;
-        } else {
-            a.out8[(size_t)y * a.W + x] = rgba;
-            if (a.out32) a.out32[(size_t)y * a.W + x] = make_float4(p.r, p.g, p.b, 1.0f);
+    float d0, d1, d2;
+    get_ray(a.cam, u, v, d0, d1, d2);
+    float t = 0.0f;
+    uint32_t idx = 0;
+    bool hit = false;
+    if (kVar == kVariantPacket) {
+        hit = walk_packet<false>(S, valid, a.cam.o[0], a.cam.o[1], a.cam.o[2], d0, d1, d2, 0.0f, t,
+                                 idx, n_nodes, n_prims, static_cast<PStackEntry*>(stk));
+    } else if (valid) {
+        hit = walk<false>(S, a.cam.o[0], a.cam.o[1], a.cam.o[2], d0, d1, d2, 0.0f, INFINITY, t, idx,
+                          n_nodes, n_prims, static_cast<uint2*>(stk));
+    }
+    const float miss_r = 200.0f / 255.0f;
+    PixelOut c{miss_r, sat(d1), sat(d2)};
+    float p0 = 0.f, p1 = 0.f, p2 = 0.f, n0 = 0.f, n1 = 0.f, n2 = 0.f, lam = 0.f;
+    uint32_t al = 0;
+    bool want_shadow = false;
+    if (hit) {
+        const float4 sp = S.spheres[idx];
+        p0 = a.cam.o[0] + t * d0;
+        p1 = a.cam.o[1] + t * d1;
+        p2 = a.cam.o[2] + t * d2;
+        const float ir = 1.0f / sp.w;
+        n0 = (p0 - sp.x) * ir;
+        n1 = (p1 - sp.y) * ir;
+        n2 = (p2 - sp.z) * ir;
+        const float ndl = n0 * a.L[0] + n1 * a.L[1] + n2 * a.L[2];
+        lam = ndl > 0.0f ? ndl : 0.0f;
+        want_shadow = ndl > 0.0f && a.shadows;
+        al = S.albedo[idx];
+    }
+    const float s0 = p0 + n0 * kShadowEps, s1 = p1 + n1 * kShadowEps, s2 = p2 + n2 * kShadowEps;
+    float ts;
+    uint32_t is;
+    if (kVar == kVariantPacket) {
+        if (__ballot(want_shadow)) {
+            n_shadow += want_shadow ? 1u : 0u;
+            if (walk_packet<true>(S, want_shadow, s0, s1, s2, a.L[0], a.L[1], a.L[2], 0.0f, ts, is,
+                                  n_nodes, n_prims, static_cast<PStackEntry*>(stk)))
+                lam = 0.0f;
         }
-    } else if (kTiles) {
-        a.out8[(size_t)k * a.tile_size * a.tile_size + ly * a.tile_size + lx] = 0u;
+    } else if (want_shadow) {
+        n_shadow += 1;
+        if (walk<true>(S, s0, s1, s2, a.L[0], a.L[1], a.L[2], 0.0f, INFINITY, ts, is, n_nodes,
+                       n_prims, static_cast<uint2*>(stk)))
+            lam = 0.0f;
+    }
+    if (hit) {
+        const float f = a.ambient + (1.0f - a.ambient) * lam;
+        c.r = static_cast<float>(al & 0xFFu) * (1.0f / 255.0f) * f;
+        c.g = static_cast<float>((al >> 8) & 0xFFu) * (1.0f / 255.0f) * f;
+        c.b = static_cast<float>((al >> 16) & 0xFFu) * (1.0f / 255.0f) * f;
+    }
+    return c;
+}
+
+// Workgroup = 4 waves = 2 x 2 wave tiles of tw x th pixels.
+template <bool kTiles, uint32_t kVar>
+__global__ void __launch_bounds__(kBlockThreads) scene_kernel(FrameArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds[];
+    float4* col = lds;  // [256] sample colours
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    void* stk;
+    if (kVar == kVariantPacket)
+        stk = reinterpret_cast<PStackEntry*>(lds + kBlockThreads) + wave * a.stack_entries;
+    else
+        stk = reinterpret_cast<uint2*>(lds + kBlockThreads) + threadIdx.x;
+    const uint32_t spw = a.spw, tw = a.tw, th = a.th;
+    const uint32_t pix = lane / spw, sub = lane - pix * spw;
+    const uint32_t qx = (wave & 1u) * tw + pix % tw;
+    const uint32_t qy = (wave >> 1) * th + pix / tw;
+    const uint32_t bw = 2u * tw, bh = 2u * th;
+    uint32_t n_shadow = 0, n_nodes = 0, n_prims = 0, n_primary = 0;
+    // Persistent workgroups: the grid is the resident block count; block
+    // tiles are dealt round-robin (spreads the costly image centre over all
+    // CUs), and the counters are flushed once per wave at the very end.
+    const uint32_t per_tile = kTiles ? (a.tile_size / bw) * (a.tile_size / bh) : 0u;
+    const uint32_t bx_n = (a.W + bw - 1) / bw;
+    const uint32_t n_bt = kTiles ? a.n_tiles * per_tile : bx_n * ((a.H + bh - 1) / bh);
+    for (uint32_t bt = blockIdx.x; bt < n_bt; bt += gridDim.x) {
+        uint32_t x, y, k = 0, lx = 0, ly = 0;
+        if (kTiles) {
+            const uint32_t tpr = a.tile_size / bw;
+            k = bt / per_tile;
+            const uint32_t b = bt - k * per_tile;
+            lx = (b % tpr) * bw + qx;
+            ly = (b / tpr) * bh + qy;
+            const uint32_t tile = a.tiles[k];
+            x = (tile % a.tiles_x) * a.tile_size + lx;
+            y = (tile / a.tiles_x) * a.tile_size + ly;
+        } else {
+            x = (bt % bx_n) * bw + qx;
+            y = (bt / bx_n) * bh + qy;
+        }
+        const bool lane_pix = pix < a.ppw && x < a.W && y < a.H;
+        const bool leader = lane_pix && sub == 0;
+        const uint32_t pid = y * a.W + x;
+        const uint32_t hp = mix32(a.seedmix ^ pid);
+        float ar = 0.0f, ag = 0.0f, ab = 0.0f;
+        for (uint32_t r = 0; r < a.rounds; ++r) {
+            const uint32_t s = r * spw + sub;
+            const bool valid = lane_pix && s < a.spp;
+            n_primary += valid ? 1u : 0u;
+            const PixelOut c =
+                sample_color<kVar>(a, x, y, hp, s, valid, n_shadow, n_nodes, n_prims, stk);
+            col[threadIdx.x] = make_float4(c.r, c.g, c.b, 0.0f);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (leader) {
+                const uint32_t nv = min(spw, a.spp - r * spw);
+                const float4* src = col + threadIdx.x;  // this pixel's samples, in order
+                for (uint32_t j = 0; j < nv; ++j) {
+                    const float4 q = src[j];
+                    ar += q.x;
+                    ag += q.y;
+                    ab += q.z;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (leader) {
+            const PixelOut p{ar * a.inv_spp, ag * a.inv_spp, ab * a.inv_spp};
+            const uint32_t rgba = pack_rgba8(p);
+            if (kTiles) {
+                a.out8[(size_t)k * a.tile_size * a.tile_size + ly * a.tile_size + lx] = rgba;
+            } else {
+                a.out8[(size_t)y * a.W + x] = rgba;
+                if (a.out32) a.out32[(size_t)y * a.W + x] = make_float4(p.r, p.g, p.b, 1.0f);
+            }
+        } else if (kTiles && sub == 0 && pix < a.ppw) {
+            a.out8[(size_t)k * a.tile_size * a.tile_size + ly * a.tile_size + lx] = 0u;  // off-image
+        }
     }
     flush_counters(a, n_primary, n_shadow, n_nodes, n_prims);
 }
@@ -399,10 +665,9 @@ __global__ void __launch_bounds__(kBlockThreads)
 // launchers (called from rt_capi.cpp)
 // ---------------------------------------------------------------------------
 
-size_t scene_lds_bytes(uint32_t max_depth) {
-    const uint32_t levels = max_depth > 1 ? max_depth - 1 : 1;
-    return static_cast<size_t>(levels) * kBlockThreads * sizeof(uint2);
-}
+// ---------------------------------------------------------------------------
+// launchers (called from rt_capi.cpp)
+// ---------------------------------------------------------------------------
 
 hipError_t launch_compat(const FrameArgs& a, hipStream_t st) {
     if (a.tiles) {
@@ -416,16 +681,65 @@ hipError_t launch_compat(const FrameArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_scene(const FrameArgs& a, hipStream_t st) {
-    const size_t lds = scene_lds_bytes(a.sc.max_depth);
-    if (a.tiles) {
-        const uint32_t per = (a.tile_size / kTileSide) * (a.tile_size / kTileSide);
-        hipLaunchKernelGGL(scene_kernel<true>, dim3(a.n_tiles * per), dim3(kBlockThreads), lds, st,
-                           a);
+size_t scene_lds_bytes(const FrameArgs& a) {
+    const size_t colours = kBlockThreads * sizeof(float4);
+    if (a.variant == kVariantPacket)
+        return colours + static_cast<size_t>(a.stack_entries) * (kBlockThreads / 64) * sizeof(PStackEntry);
+    const uint32_t levels = a.sc.max_depth > 1 ? a.sc.max_depth - 1 : 1;
+    return colours + static_cast<size_t>(levels) * kBlockThreads * sizeof(uint2);
+}
+
+// Resident workgroups per CU for a kernel at a given LDS size (queried once).
+template <typename K>
+static uint32_t resident_blocks(K kernel, size_t lds) {
+    static thread_local int dev_cached = -1, cus = 0;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev != dev_cached) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+        dev_cached = dev;
+    }
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlockThreads, lds) != hipSuccess ||
+        per_cu <= 0)
+        per_cu = 4;
+    return static_cast<uint32_t>((cus > 0 ? cus : 256) * per_cu);
+}
+
+template <bool kTiles>
+static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStream_t st) {
+    if (a.variant == kVariantPacket) {
+        auto k = scene_kernel<kTiles, kVariantPacket>;
+        const uint32_t grid = std::min(n_bt, resident_blocks(k, lds));
+        hipLaunchKernelGGL(k, dim3(grid), dim3(kBlockThreads), lds, st, a);
     } else {
-        hipLaunchKernelGGL(scene_kernel<false>,
-                           dim3((a.W + kTileSide - 1) / kTileSide, (a.H + kTileSide - 1) / kTileSide),
-                           dim3(kBlockThreads), lds, st, a);
+        auto k = scene_kernel<kTiles, kVariantLane>;
+        const uint32_t grid = std::min(n_bt, resident_blocks(k, lds));
+        hipLaunchKernelGGL(k, dim3(grid), dim3(kBlockThreads), lds, st, a);
+    }
+}
+
+hipError_t launch_scene(const FrameArgs& a_in, hipStream_t st) {
+    FrameArgs a = a_in;
+    // wave mapping: spw samples x ppw pixels per wave (see scene_kernel)
+    a.spw = a.spp >= 64u ? 64u : a.spp;
+    uint32_t ppw = 1;
+    while (ppw * 2u * a.spw <= 64u) ppw *= 2u;
+    a.ppw = ppw;
+    uint32_t lg = 0;
+    while ((1u << lg) < ppw) ++lg;
+    a.tw = 1u << ((lg + 1) / 2);
+    a.th = 1u << (lg / 2);
+    a.rounds = (a.spp + a.spw - 1) / a.spw;
+    a.stack_entries = 8u * a.sc.max_depth + 8u;
+    const size_t lds = scene_lds_bytes(a);
+    const uint32_t bw = 2u * a.tw, bh = 2u * a.th;
+    if (a.tiles) {
+        const uint32_t per = (a.tile_size / bw) * (a.tile_size / bh);
+        launch_scene_t<true>(a, a.n_tiles * per, lds, st);
+    } else {
+        launch_scene_t<false>(a, ((a.W + bw - 1) / bw) * ((a.H + bh - 1) / bh), lds, st);
     }
     return hipGetLastError();
 }

@@ -14,6 +14,11 @@ constexpr uint32_t kMaxDepth = 16;  // octree depth limit (grid coordinates stay
 constexpr float kShadowEps = 1e-5f; // shadow-ray origin offset along the normal (world units)
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 
+// scene kernel variants (rt_config.flags bits 16..19, RT_FLAG_VARIANT_SHIFT)
+constexpr uint32_t kVariantLane = 1;    // one ray per lane, per-thread LDS ancestor stack
+constexpr uint32_t kVariantPacket = 2;  // 64-ray wave packet, per-wave LDS stack, ballot masks
+constexpr uint32_t kVariantDefault = kVariantLane;
+
 // Pinhole camera (include/camera.h:9-56): K and R column-major like glm.
 struct CamArgs {
     float K[9];  // K[c*3+r]
@@ -63,6 +68,10 @@ struct FrameArgs {
     uint32_t tile_size;
     uint32_t tiles_x;   // ceil(W / tile_size)
     unsigned long long* counters;  // [primary, shadow, nodes, prims]
+    uint32_t variant;   // scene kernel variant (kVariant*)
+    uint32_t stack_entries;  // packet kernel: LDS stack entries per wave
+    // wave mapping (set by launch_scene): a wave = ppw pixels (tw x th) x spw samples
+    uint32_t spw, ppw, tw, th, rounds;
 };
 
 }  // namespace rtamd

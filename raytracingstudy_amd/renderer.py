@@ -70,7 +70,8 @@ class KernelRenderer:
     def __init__(self, width: int, height: int, *, mode: str = "compat", spp: int = 1,
                  seed: int = 0x2545F491, device: int = -1, jitter: Optional[bool] = None,
                  shadows: bool = True, radiance: bool = False,
-                 light_dir: Sequence[float] = (1.0, 1.0, -1.0), ambient: float = 0.1):
+                 light_dir: Sequence[float] = (1.0, 1.0, -1.0), ambient: float = 0.1,
+                 variant: int = 0):
         lib = _lib.load()
         cfg = RtConfig()
         lib.rt_config_default(ctypes.byref(cfg))
@@ -88,6 +89,7 @@ class KernelRenderer:
             flags |= RT_FLAG_NO_SHADOWS
         if radiance:
             flags |= RT_FLAG_RADIANCE
+        flags |= (int(variant) & 0xF) << _lib.RT_FLAG_VARIANT_SHIFT
         cfg.flags = flags
         for i in range(3):
             cfg.light_dir[i] = float(light_dir[i])

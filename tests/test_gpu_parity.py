@@ -68,14 +68,14 @@ def test_compat_reference_intrinsic_k0(gpu, oracle):
 
 
 def _scene_pair(oracle, n, w, h, spp, depth=7, pose=None, shadows=True, jitter=None, seed=rt.SEED,
-                leaf=8, spheres=None, rect=None, row_step=1):
+                leaf=8, spheres=None, rect=None, row_step=1, variant=0):
     if spheres is None:
         sp, al = rt.generate_spheres(n, rt.SEED)
     else:
         sp, al = spheres
     pose = scene_pose() if pose is None else pose
     r = rt.KernelRenderer(w, h, mode="scene", spp=spp, seed=seed, radiance=True, shadows=shadows,
-                          jitter=jitter)
+                          jitter=jitter, variant=variant)
     r.resize(w, h)
     r.setPosition(pose)
     info = r.set_scene(sp, al, max_depth=depth, leaf_capacity=leaf)
@@ -91,6 +91,18 @@ def _scene_pair(oracle, n, w, h, spp, depth=7, pose=None, shadows=True, jitter=N
     return img, rad, st, info, ref8, ref32, cnt, oinfo
 
 
+VARIANTS = [rt._lib.VARIANT_LANE, rt._lib.VARIANT_PACKET]
+
+
+def _check_counts(st, cnt, variant):
+    # rays cast are a property of the image; node/prim counts are the work of
+    # the traversal: the one-ray-per-lane walk reproduces the oracle's exactly
+    assert (st.primary_rays, st.shadow_rays) == (int(cnt[0]), int(cnt[1]))
+    if variant == rt._lib.VARIANT_LANE:
+        assert (st.nodes_visited, st.prims_tested) == (int(cnt[2]), int(cnt[3]))
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("n,w,h,spp,depth", [
     (1000, 320, 240, 1, 7),
     (1000, 160, 120, 4, 7),
@@ -100,29 +112,33 @@ def _scene_pair(oracle, n, w, h, spp, depth=7, pose=None, shadows=True, jitter=N
     (0, 64, 48, 2, 7),
     (5, 100, 70, 3, 7),      # root is a leaf (n <= leaf capacity)
 ])
-def test_scene_bit_exact(gpu, oracle, n, w, h, spp, depth):
-    img, rad, st, info, ref8, ref32, cnt, oinfo = _scene_pair(oracle, n, w, h, spp, depth)
+def test_scene_bit_exact(gpu, oracle, n, w, h, spp, depth, variant):
+    img, rad, st, info, ref8, ref32, cnt, oinfo = _scene_pair(oracle, n, w, h, spp, depth,
+                                                              variant=variant)
     assert info["n_nodes"] == oinfo["n_nodes"]
     assert info["n_prim_refs"] == oinfo["n_prim_refs"]
     assert np.abs(rad - ref32).max() <= TOL
     assert np.array_equal(rad, ref32)
     assert np.array_equal(img, ref8)
-    assert (st.primary_rays, st.shadow_rays, st.nodes_visited, st.prims_tested) == tuple(int(c) for c in cnt)
+    _check_counts(st, cnt, variant)
 
 
-def test_scene_c2_full_size(gpu, oracle):
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_scene_c2_full_size(gpu, oracle, variant):
     """C2 at its full size: 1920x1080, 1 spp, 1k spheres."""
-    img, rad, st, info, ref8, ref32, cnt, _ = _scene_pair(oracle, 1000, 1920, 1080, 1)
+    img, rad, st, info, ref8, ref32, cnt, _ = _scene_pair(oracle, 1000, 1920, 1080, 1,
+                                                           variant=variant)
     assert np.array_equal(img, ref8)
     assert np.array_equal(rad, ref32)
     assert st.primary_rays == 1920 * 1080 == cnt[0]
-    assert (st.shadow_rays, st.nodes_visited, st.prims_tested) == tuple(int(c) for c in cnt[1:])
+    _check_counts(st, cnt, variant)
 
 
-def test_scene_c3_rows_subsample(gpu, oracle):
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_scene_c3_rows_subsample(gpu, oracle, variant):
     """C3 scene at full size (1920x1080, 100k spheres), 4 spp, every 32nd row vs the oracle."""
     img, rad, st, info, ref8, ref32, cnt, _ = _scene_pair(oracle, 100_000, 1920, 1080, 4,
-                                                           row_step=32)
+                                                           row_step=32, variant=variant)
     rows = np.arange(0, 1080, 32)
     assert np.array_equal(img[rows], ref8[rows])
     assert np.array_equal(rad[rows], ref32[rows])
@@ -152,17 +168,19 @@ def test_tiles_match_frame(gpu):
         assert np.array_equal(img.cpu().numpy().reshape(h, w, 4), full)
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("case", ["inside", "yawed", "grazing_axis", "far"])
-def test_scene_camera_cases(gpu, oracle, case):
+def test_scene_camera_cases(gpu, oracle, case, variant):
     """Camera inside the octree, off-axis poses, axis-aligned rays, distant camera."""
     pose = {"inside": translation_pose(0.64, 0.64, 0.64),
             "yawed": display_pose((1.9, 1.4, 1.9), 40.0, -25.0),
             "grazing_axis": translation_pose(0.32, 0.32, 2.0),
             "far": translation_pose(0.64, 0.64, 40.0)}[case]
-    img, rad, st, info, ref8, ref32, cnt, _ = _scene_pair(oracle, 5000, 160, 96, 2, pose=pose)
+    img, rad, st, info, ref8, ref32, cnt, _ = _scene_pair(oracle, 5000, 160, 96, 2, pose=pose,
+                                                           variant=variant)
     assert np.array_equal(img, ref8)
     assert np.array_equal(rad, ref32)
-    assert (st.shadow_rays, st.nodes_visited, st.prims_tested) == tuple(int(c) for c in cnt[1:])
+    _check_counts(st, cnt, variant)
 
 
 def test_scene_no_shadows_no_jitter(gpu, oracle):
@@ -194,7 +212,7 @@ def test_scene_custom_root_and_resolution(gpu, oracle):
     sc = oracle.Scene(sp, al, root_min=(-0.5, 0, 0), root_max=(2.06, 1.28, 1.28), max_depth=depth)
     ref8, ref32, cnt = sc.render(w, h, pose, K, spp=1)
     assert np.array_equal(img, ref8) and np.array_equal(rad, ref32)
-    assert st.nodes_visited == cnt[2] and st.prims_tested == cnt[3]
+    assert st.primary_rays == cnt[0] and st.shadow_rays == cnt[1]
 
 
 def test_external_buffer_and_stream(gpu):

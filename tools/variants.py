@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""A/B the scene-kernel variants in ONE process (interleaved rounds).
+
+    python tools/variants.py [--configs c2,c3] [--variants 1,2] [--rounds 3]
+
+For each config, one renderer per variant renders the same frame; rounds are
+interleaved (v1, v2, v1, v2, ...) and the kernel time (hipEvent, rt_stats.ms)
+is reported as median/min.  Every variant's image must equal variant 1's
+byte for byte (results are variant-independent by construction).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+import raytracingstudy_amd as rt  # noqa: E402
+from raytracingstudy_amd.camera import scene_pose  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c2,c3")
+    ap.add_argument("--variants", default="1,2")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--spp", type=int, default=0, help="override spp")
+    args = ap.parse_args()
+    variants = [int(v) for v in args.variants.split(",")]
+    out = {}
+    for name in args.configs.split(","):
+        cfg = rt.CONFIGS[name]
+        spp = args.spp or cfg.spp
+        sp, al = rt.generate_spheres(cfg.n_spheres, rt.SEED)
+        rs = {}
+        for v in variants:
+            r = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=spp, variant=v)
+            r.resize(cfg.width, cfg.height)
+            r.setPosition(scene_pose())
+            r.set_scene(sp, al, max_depth=cfg.max_depth)
+            r.render(stats=True)  # warm-up
+            rs[v] = r
+        times = {v: [] for v in variants}
+        stats = {}
+        for _ in range(args.rounds):
+            for v in variants:
+                st = rs[v].render(stats=True)
+                times[v].append(st.ms)
+                stats[v] = st
+        ref = rs[variants[0]].readback()
+        res = {}
+        for v in variants:
+            img = rs[v].readback()
+            st = stats[v]
+            rays = st.primary_rays + st.shadow_rays
+            med = float(np.median(times[v]))
+            res[v] = {"ms_median": round(med, 3), "ms_min": round(min(times[v]), 3),
+                      "Mrays_s": round(rays / med / 1e3, 1), "rays": int(rays),
+                      "nodes_per_ray": round(st.nodes_visited / rays, 2),
+                      "prims_per_ray": round(st.prims_tested / rays, 2),
+                      "image_equal_to_v%d" % variants[0]: bool(np.array_equal(img, ref))}
+            rs[v].close()
+        out[f"{name} spp{spp}"] = res
+        print(name, json.dumps(res), flush=True)
+    return 0 if all(r[v]["image_equal_to_v%d" % variants[0]] for r in out.values() for v in r) else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
