@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU-baseline sample duration")
+    ap.add_argument("--variant", type=int, default=0, help="scene-kernel variant (0 = default)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="PMC traffic summary written by tools/pmc_traffic.py")
     return ap.parse_args()
@@ -97,7 +98,8 @@ def main():
 
     sp, al = rt.generate_spheres(cfg.n_spheres, rt.SEED)
     r = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=cfg.spp, device=local,
-                          light_dir=rt.configs.LIGHT_DIR, ambient=rt.configs.AMBIENT)
+                          light_dir=rt.configs.LIGHT_DIR, ambient=rt.configs.AMBIENT,
+                          variant=args.variant)
     r.resize(cfg.width, cfg.height)
     pose = scene_pose()
     r.setPosition(pose)

@@ -370,18 +370,20 @@ void orc_scene_root(const orc_scene* s, float rmin[3], float rmax[3]) {
 /* ---- ray / sphere ---------------------------------------------------------- */
 
 /* Nearest root of |o + t d - c| = r with the perpendicular-distance
- * discriminant (no b*b - c cancellation); accepted iff tmin < t < tmax. */
+ * discriminant (no b*b - c cancellation), written with explicit fmaf so the
+ * kernel evaluates the identical operations; accepted iff tmin < t < tmax. */
 static inline int isect(const float o[3], const float d[3], const float* sp, float tmin,
                         float tmax, float* tout) {
     const float ocx = o[0] - sp[0];
     const float ocy = o[1] - sp[1];
     const float ocz = o[2] - sp[2];
-    const float b = ocx * d[0] + ocy * d[1] + ocz * d[2];
-    const float qx = ocx - b * d[0];
-    const float qy = ocy - b * d[1];
-    const float qz = ocz - b * d[2];
+    const float b = fmaf(ocz, d[2], fmaf(ocy, d[1], ocx * d[0]));
+    const float qx = fmaf(-b, d[0], ocx);
+    const float qy = fmaf(-b, d[1], ocy);
+    const float qz = fmaf(-b, d[2], ocz);
+    const float qq = fmaf(qz, qz, fmaf(qy, qy, qx * qx));
     const float r = sp[3];
-    const float h = r * r - (qx * qx + qy * qy + qz * qz);
+    const float h = fmaf(r, r, -qq);
     if (h < 0.0f) return 0;
     const float sq = sqrtf(h);
     float t = -b - sq;
@@ -396,11 +398,13 @@ static inline int isect(const float o[3], const float d[3], const float* sp, flo
 typedef struct {
     float og[3];   /* origin in (mirrored) grid units */
     float inv[3];  /* 1 / (|d| * scale), |d| clamped to >= 1e-20 */
+    float nog[3];  /* -(og * inv) */
     uint32_t mask; /* bit i: axis i mirrored (d_i < 0) */
 } walk_t;
 
+/* t of the grid plane at (mirrored) integer coordinate k: one FMA, monotone in k */
 static inline float plane(const walk_t* w, int i, uint32_t k) {
-    return ((float)k - w->og[i]) * w->inv[i];
+    return fmaf((float)k, w->inv[i], w->nog[i]);
 }
 
 static int walk(const orc_scene* s, const float o[3], const float d[3], float tmin, float tmax,
@@ -415,6 +419,7 @@ static int walk(const orc_scene* s, const float o[3], const float d[3], float tm
         if (a < 1e-20f) a = 1e-20f;
         w.og[i] = neg ? s->G - g : g;
         w.inv[i] = 1.0f / (a * s->scale[i]);
+        w.nog[i] = -(w.og[i] * w.inv[i]);
         w.mask |= (uint32_t)neg << i;
     }
     float t0 = plane(&w, 0, 0), t1 = plane(&w, 0, G);

@@ -231,7 +231,8 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : r->stream;
     if (r->cfg.mode == RT_MODE_SCENE && !r->has_scene)
         return fail(r, RT_E_NOSCENE, "RT_MODE_SCENE render without rt_set_scene");
-    RT_HIP(r, hipMemsetAsync(r->counters.p, 0, 4 * sizeof(unsigned long long), st));
+    RT_HIP(r, hipMemsetAsync(r->counters.p, 0, kCounterWords * sizeof(unsigned long long), st));
+    a.count_work = stats ? 1u : 0u;
     if (stats) RT_HIP(r, hipEventRecord(r->ev0, st));
     hipError_t e = r->cfg.mode == RT_MODE_SCENE ? launch_scene(a, st) : launch_compat(a, st);
     if (e != hipSuccess) return hip_fail(r, e, "kernel launch");
@@ -337,7 +338,7 @@ int rt_create(const rt_config* cfg, rt_renderer** out) {
         return st;
     }
     if ((st = ensure(r, r->fb, (size_t)r->W * r->H)) ||
-        (st = ensure(r, r->counters, 4))) {
+        (st = ensure(r, r->counters, kCounterWords))) {
         g_last_error = r->err;
         rt_destroy(r);
         return st;

@@ -12,6 +12,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
+#include <utility>
+#include <vector>
 
 #include "rt_params.h"
 
@@ -107,17 +110,20 @@ __global__ void __launch_bounds__(kBlockThreads) compat_tiles_kernel(FrameArgs a
 // Scene mode
 // ---------------------------------------------------------------------------
 
-// Nearest root with the perpendicular-distance discriminant; tmin < t < tmax.
+// Nearest root with the perpendicular-distance discriminant, explicit FMAs
+// (13 VALU to the h < 0 test); accepted iff tmin < t < tmax.  Same operations
+// as oracle.c:isect.
 __device__ __forceinline__ bool isect(float o0, float o1, float o2, float d0, float d1, float d2,
                                       float4 sp, float tmin, float tmax, float& tout) {
     const float ocx = o0 - sp.x;
     const float ocy = o1 - sp.y;
     const float ocz = o2 - sp.z;
-    const float b = ocx * d0 + ocy * d1 + ocz * d2;
-    const float qx = ocx - b * d0;
-    const float qy = ocy - b * d1;
-    const float qz = ocz - b * d2;
-    const float h = sp.w * sp.w - (qx * qx + qy * qy + qz * qz);
+    const float b = fmaf(ocz, d2, fmaf(ocy, d1, ocx * d0));
+    const float qx = fmaf(-b, d0, ocx);
+    const float qy = fmaf(-b, d1, ocy);
+    const float qz = fmaf(-b, d2, ocz);
+    const float qq = fmaf(qz, qz, fmaf(qy, qy, qx * qx));
+    const float h = fmaf(sp.w, sp.w, -qq);
     if (h < 0.0f) return false;
     const float sq = sqrtf(h);
     float t = -b - sq;
@@ -133,15 +139,22 @@ __device__ __forceinline__ bool isect(float o0, float o1, float o2, float d0, fl
 // mid-plane tests at the current t, leave a cell through its exit planes, and
 // pop to the common ancestor found from the highest flipped coordinate bit.
 // The per-thread ancestor stack lives in LDS, [depth-1][thread] (conflict-free).
-template <bool kAnyHit>
+// kAnyHit: compile-time any-hit; with kDynAny the mode comes from `any_rt`
+// instead, so ONE inlined walk serves both the primary and the shadow ray.
+template <bool kAnyHitT, int kChunk = 4, bool kUni = false, bool kDynAny = false,
+          bool kStats = true>
 __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, float o2, float d0,
                                      float d1, float d2, float tmin, float tmax, float& tout,
                                      uint32_t& iout, uint32_t& n_nodes, uint32_t& n_prims,
-                                     uint2* __restrict__ stk) {
-    const uint32_t G = 1u << S.max_depth;
+                                     uint2* __restrict__ stk, bool any_rt = false) {
+    const bool kAnyHit = kDynAny ? any_rt : kAnyHitT;
+    const uint32_t D = S.max_depth;
+    const uint32_t G = 1u << D;
+    const float4* __restrict__ prim_sp = S.prim_sp;
+    const uint2* __restrict__ nodes = S.nodes;
     const float o[3] = {o0, o1, o2};
     const float d[3] = {d0, d1, d2};
-    float og[3], inv[3];
+    float inv[3], nog[3];
     uint32_t mask = 0;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -149,11 +162,13 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         const bool neg = d[i] < 0.0f;
         float a = fabsf(d[i]);
         if (a < 1e-20f) a = 1e-20f;
-        og[i] = neg ? S.G - g : g;
+        const float og = neg ? S.G - g : g;
         inv[i] = 1.0f / (a * S.scale[i]);
+        nog[i] = -(og * inv[i]);
         mask |= static_cast<uint32_t>(neg) << i;
     }
-    auto plane = [&](int i, uint32_t k) { return (static_cast<float>(k) - og[i]) * inv[i]; };
+    // t of the grid plane at (mirrored) integer k: one FMA (oracle.c:plane)
+    auto plane = [&](int i, uint32_t k) { return fmaf(static_cast<float>(k), inv[i], nog[i]); };
     float t0 = plane(0, 0), t1 = plane(0, G);
 #pragma unroll
     for (int i = 1; i < 3; ++i) {
@@ -166,25 +181,62 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
     if (!(t0 < t1)) return false;
 
     float best_t = tmax;
-    uint32_t best = kNoHit;
-    n_nodes += 1;
+    if (kStats) n_nodes += 1;
 
-    auto leaf = [&](uint32_t off, uint32_t cnt) -> bool {
-        for (uint32_t j = 0; j < cnt; ++j) {
-            const float4 sp = S.prim_sp[off + j];
-            n_prims += 1;
-            float th;
-            if (isect(o0, o1, o2, d0, d1, d2, sp, tmin, tmax, th)) {
-                if (kAnyHit) {
-                    tout = th;
-                    return true;
-                }
-                const uint32_t idx = S.prim_idx[off + j];
-                if (th < best_t || (th == best_t && idx < best)) {
-                    best_t = th;
-                    best = idx;
-                }
+    // Nearest keeps the best leaf *reference*; the sphere index is loaded only
+    // for an exact t tie (rare) and once at the end, so no dependent load sits
+    // in the hot loop.  Same result as the oracle's (min t, then min index).
+    uint32_t best_ref = kNoHit;
+    auto test = [&](const float4& sp, uint32_t ref) -> bool {
+        if (kStats) n_prims += 1;
+        float th;
+        if (isect(o0, o1, o2, d0, d1, d2, sp, tmin, tmax, th)) {
+            if (kAnyHit) {
+                tout = th;
+                return true;
             }
+            if (th < best_t) {
+                best_t = th;
+                best_ref = ref;
+            } else if (th == best_t && S.prim_idx[ref] < S.prim_idx[best_ref]) {
+                best_ref = ref;
+            }
+        }
+        return false;
+    };
+    // Leaf spheres in list order (same order, hence same counters, as the
+    // oracle).  kUni: when every active lane sits in the same leaf (the usual
+    // case: a wave traces the samples of one pixel) the spheres are read with
+    // wave-uniform (scalar) loads and broadcast; otherwise each lane loads its
+    // own, kChunk loads in flight.
+    auto leaf = [&](uint32_t off, uint32_t cnt) -> bool {
+        if (kUni) {
+            const uint32_t uoff = __builtin_amdgcn_readfirstlane(off);
+            if (__all(off == uoff)) {
+                const uint32_t ucnt = __builtin_amdgcn_readfirstlane(cnt);
+                bool alive = true, hit = false;
+                for (uint32_t j = 0; j < ucnt; ++j) {
+                    const float4 sp = prim_sp[uoff + j];
+                    if (alive && test(sp, uoff + j)) {
+                        alive = false;
+                        hit = true;
+                    }
+                    if (kAnyHit && !__any(alive)) break;
+                }
+                return hit;
+            }
+        }
+        const float4* __restrict__ ps = prim_sp + off;
+        const uint32_t last = cnt - 1;
+        for (uint32_t j = 0; j < cnt; j += kChunk) {
+            const uint32_t m = cnt - j;
+            // unconditional loads clamped to the leaf: kChunk dwordx4 in flight
+            float4 sv[kChunk];
+#pragma unroll
+            for (int q = 0; q < kChunk; ++q) sv[q] = ps[min(j + q, last)];
+#pragma unroll
+            for (int q = 0; q < kChunk; ++q)
+                if (m > static_cast<uint32_t>(q) && test(sv[q], off + j + q)) return true;
         }
         return false;
     };
@@ -198,11 +250,11 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         // Hard cap (never reached by a correct walk: a ray crosses < 3*G cells
         // and each crossing costs at most one descent): no input can hang the GPU.
         for (uint32_t it = 0, cap = 8u * G + 64u; it < cap; ++it) {
-            const uint32_t half = G >> (depth + 1);
+            const uint32_t hs = D - depth - 1u;  // log2 of the half cell size
             uint32_t bits = 0;
-            if (plane(0, (2u * c0 + 1u) * half) <= t) bits |= 1u;
-            if (plane(1, (2u * c1 + 1u) * half) <= t) bits |= 2u;
-            if (plane(2, (2u * c2 + 1u) * half) <= t) bits |= 4u;
+            if (plane(0, (2u * c0 + 1u) << hs) <= t) bits |= 1u;
+            if (plane(1, (2u * c1 + 1u) << hs) <= t) bits |= 2u;
+            if (plane(2, (2u * c2 + 1u) << hs) <= t) bits |= 4u;
             const uint32_t child = bits ^ mask;
             c0 = 2u * c0 + (bits & 1u);
             c1 = 2u * c1 + ((bits >> 1) & 1u);
@@ -211,8 +263,14 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             const uint32_t valid = node.y & 0xFFu;
             if (valid & (1u << child)) {
                 const uint32_t slot = node.x + __builtin_popcount(valid & ((1u << child) - 1u));
-                const uint2 rec = S.nodes[slot];
-                n_nodes += 1;
+                uint2 rec;
+                if (kUni) {
+                    const uint32_t uslot = __builtin_amdgcn_readfirstlane(slot);
+                    rec = __all(slot == uslot) ? nodes[uslot] : nodes[slot];
+                } else {
+                    rec = nodes[slot];
+                }
+                if (kStats) n_nodes += 1;
                 if (!((node.y >> 8) & (1u << child))) {
                     node = rec;
                     stk[(depth - 1) * kBlockThreads] = rec;
@@ -220,10 +278,10 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 }
                 if (leaf(rec.x, rec.y)) return true;
             }
-            const uint32_t size = G >> depth;
-            const float e0 = plane(0, (c0 + 1u) * size);
-            const float e1 = plane(1, (c1 + 1u) * size);
-            const float e2 = plane(2, (c2 + 1u) * size);
+            const uint32_t ls = D - depth;  // log2 of the cell size
+            const float e0 = plane(0, (c0 + 1u) << ls);
+            const float e1 = plane(1, (c1 + 1u) << ls);
+            const float e2 = plane(2, (c2 + 1u) << ls);
             float texit = e0 < e1 ? e0 : e1;
             texit = texit < e2 ? texit : e2;
             if (!kAnyHit && best_t < texit) break;
@@ -244,9 +302,9 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             t = texit;
         }
     }
-    if (!kAnyHit && best != kNoHit) {
+    if (!kAnyHit && best_ref != kNoHit) {
         tout = best_t;
-        iout = best;
+        iout = S.prim_idx[best_ref];
         return true;
     }
     return false;
@@ -291,7 +349,7 @@ __device__ __forceinline__ bool walk_packet(const SceneArgs& S, bool want, float
     const uint32_t G = 1u << S.max_depth;
     const float o[3] = {o0, o1, o2};
     const float d[3] = {d0, d1, d2};
-    float og[3], inv[3];
+    float inv[3], nog[3];
     bool mir[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -299,15 +357,13 @@ __device__ __forceinline__ bool walk_packet(const SceneArgs& S, bool want, float
         mir[i] = d[i] < 0.0f;
         float a = fabsf(d[i]);
         if (a < 1e-20f) a = 1e-20f;
-        og[i] = mir[i] ? S.G - g : g;
+        const float og = mir[i] ? S.G - g : g;
         inv[i] = 1.0f / (a * S.scale[i]);
+        nog[i] = -(og * inv[i]);
     }
+    auto plane_m = [&](int i, uint32_t km) { return fmaf(static_cast<float>(km), inv[i], nog[i]); };
     // t of the plane at REAL grid coordinate k, in this lane's mirrored frame
-    auto P = [&](int i, uint32_t k) {
-        const uint32_t km = mir[i] ? G - k : k;
-        return (static_cast<float>(km) - og[i]) * inv[i];
-    };
-    auto plane_m = [&](int i, uint32_t km) { return (static_cast<float>(km) - og[i]) * inv[i]; };
+    auto P = [&](int i, uint32_t k) { return plane_m(i, mir[i] ? G - k : k); };
     float t0 = plane_m(0, 0), t1 = plane_m(0, G);
 #pragma unroll
     for (int i = 1; i < 3; ++i) {
@@ -496,7 +552,7 @@ __device__ __forceinline__ void flush_counters(const FrameArgs& a, uint32_t prim
 // One sample of pixel (x, y): primary walk, Lambert shade, shadow walk.
 // kVar selects the traversal; `valid` lanes trace, the others only take part
 // in the packet walks' wave-wide votes.
-template <uint32_t kVar>
+template <uint32_t kVar, int kChunk, bool kUni>
 __device__ __forceinline__ PixelOut sample_color(const FrameArgs& a, uint32_t x, uint32_t y,
                                                  uint32_t hp, uint32_t s, bool valid,
                                                  uint32_t& n_shadow, uint32_t& n_nodes,
@@ -516,8 +572,8 @@ __device__ __forceinline__ PixelOut sample_color(const FrameArgs& a, uint32_t x,
         hit = walk_packet<false>(S, valid, a.cam.o[0], a.cam.o[1], a.cam.o[2], d0, d1, d2, 0.0f, t,
                                  idx, n_nodes, n_prims, static_cast<PStackEntry*>(stk));
     } else if (valid) {
-        hit = walk<false>(S, a.cam.o[0], a.cam.o[1], a.cam.o[2], d0, d1, d2, 0.0f, INFINITY, t, idx,
-                          n_nodes, n_prims, static_cast<uint2*>(stk));
+        hit = walk<false, kChunk, kUni>(S, a.cam.o[0], a.cam.o[1], a.cam.o[2], d0, d1, d2, 0.0f, INFINITY,
+                                  t, idx, n_nodes, n_prims, static_cast<uint2*>(stk));
     }
     const float miss_r = 200.0f / 255.0f;
     PixelOut c{miss_r, sat(d1), sat(d2)};
@@ -550,8 +606,8 @@ __device__ __forceinline__ PixelOut sample_color(const FrameArgs& a, uint32_t x,
         }
     } else if (want_shadow) {
         n_shadow += 1;
-        if (walk<true>(S, s0, s1, s2, a.L[0], a.L[1], a.L[2], 0.0f, INFINITY, ts, is, n_nodes,
-                       n_prims, static_cast<uint2*>(stk)))
+        if (walk<true, kChunk, kUni>(S, s0, s1, s2, a.L[0], a.L[1], a.L[2], 0.0f, INFINITY, ts, is,
+                               n_nodes, n_prims, static_cast<uint2*>(stk)))
             lam = 0.0f;
     }
     if (hit) {
@@ -563,84 +619,182 @@ __device__ __forceinline__ PixelOut sample_color(const FrameArgs& a, uint32_t x,
     return c;
 }
 
-// Workgroup = 4 waves = 2 x 2 wave tiles of tw x th pixels.
-template <bool kTiles, uint32_t kVar>
-__global__ void __launch_bounds__(kBlockThreads) scene_kernel(FrameArgs a) {
+// Unified lane path: one walk instance run twice (primary, then the shadow ray
+// of the lanes that need one), so the register allocator sees one walk.
+template <int kChunk, bool kStats>
+__device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uint32_t x,
+                                                         uint32_t y, uint32_t hp, uint32_t s,
+                                                         bool valid, uint32_t& n_shadow,
+                                                         uint32_t& n_nodes, uint32_t& n_prims,
+                                                         void* stk) {
+    const SceneArgs& S = a.sc;
+    float u = static_cast<float>(x), v = static_cast<float>(y);
+    if (a.jitter) {
+        u = u + u01(mix32(hp ^ (s << 1)));
+        v = v + u01(mix32(hp ^ ((s << 1) | 1u)));
+    }
+    float r0 = a.cam.o[0], r1 = a.cam.o[1], r2 = a.cam.o[2];
+    float d0, d1, d2;
+    get_ray(a.cam, u, v, d0, d1, d2);
+    const float miss_g = sat(d1), miss_b = sat(d2);
+    bool active = valid, any = false, hit0 = false;
+    float lam = 0.0f;
+    uint32_t al = 0;
+    for (int phase = 0; phase < 2; ++phase) {
+        float t = 0.0f;
+        uint32_t idx = 0;
+        bool hit = false;
+        if (active)
+            hit = walk<false, kChunk, false, true, kStats>(S, r0, r1, r2, d0, d1, d2, 0.0f, INFINITY,
+                                                           t, idx, n_nodes, n_prims,
+                                                           static_cast<uint2*>(stk), any);
+        if (phase == 0) {
+            hit0 = active && hit;
+            bool want_shadow = false;
+            if (hit0) {
+                const float4 sp = S.spheres[idx];
+                const float p0 = r0 + t * d0;
+                const float p1 = r1 + t * d1;
+                const float p2 = r2 + t * d2;
+                const float ir = 1.0f / sp.w;
+                const float n0 = (p0 - sp.x) * ir;
+                const float n1 = (p1 - sp.y) * ir;
+                const float n2 = (p2 - sp.z) * ir;
+                const float ndl = n0 * a.L[0] + n1 * a.L[1] + n2 * a.L[2];
+                lam = ndl > 0.0f ? ndl : 0.0f;
+                want_shadow = ndl > 0.0f && a.shadows;
+                al = S.albedo[idx];
+                r0 = p0 + n0 * kShadowEps;
+                r1 = p1 + n1 * kShadowEps;
+                r2 = p2 + n2 * kShadowEps;
+                d0 = a.L[0];
+                d1 = a.L[1];
+                d2 = a.L[2];
+            }
+            active = want_shadow;
+            any = true;
+            n_shadow += active ? 1u : 0u;
+            if (!__any(active)) break;
+        } else if (active && hit) {
+            lam = 0.0f;
+        }
+    }
+    PixelOut c{200.0f / 255.0f, miss_g, miss_b};
+    if (hit0) {
+        const float f = a.ambient + (1.0f - a.ambient) * lam;
+        c.r = static_cast<float>(al & 0xFFu) * (1.0f / 255.0f) * f;
+        c.g = static_cast<float>((al >> 8) & 0xFFu) * (1.0f / 255.0f) * f;
+        c.b = static_cast<float>((al >> 16) & 0xFFu) * (1.0f / 255.0f) * f;
+    }
+    return c;
+}
+
+// Persistent workgroups pull 16x16-pixel block tiles from a device-wide
+// atomic queue (one returning atomic per tile; counters[kQueueSlot], zeroed
+// with the counters before every launch); the tile's wave tiles (tw x th
+// pixels, see launch_scene) are dealt to the 4 waves round-robin.  Neighbour
+// pixels run on one CU (L1 reuse) and the queue balances costly image regions.
+// kMinW = minimum waves per SIMD requested from the register allocator.
+template <bool kTiles, uint32_t kVar, int kMinW, int kChunk, bool kUni, bool kStats = true>
+__global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
-    float4* col = lds;  // [256] sample colours
+    float4* col = lds;                  // [256] sample colours
+    float4* acc = lds + kBlockThreads;  // [256] running pixel sums (leader lanes' slots)
+    __shared__ uint32_t tile_slot;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     void* stk;
     if (kVar == kVariantPacket)
-        stk = reinterpret_cast<PStackEntry*>(lds + kBlockThreads) + wave * a.stack_entries;
+        stk = reinterpret_cast<PStackEntry*>(lds + 2 * kBlockThreads) + wave * a.stack_entries;
     else
-        stk = reinterpret_cast<uint2*>(lds + kBlockThreads) + threadIdx.x;
+        stk = reinterpret_cast<uint2*>(lds + 2 * kBlockThreads) + threadIdx.x;
     const uint32_t spw = a.spw, tw = a.tw, th = a.th;
     const uint32_t pix = lane / spw, sub = lane - pix * spw;
-    const uint32_t qx = (wave & 1u) * tw + pix % tw;
-    const uint32_t qy = (wave >> 1) * th + pix / tw;
-    const uint32_t bw = 2u * tw, bh = 2u * th;
+    const uint32_t wtx = kTileSide / tw, wtiles = wtx * (kTileSide / th);
     uint32_t n_shadow = 0, n_nodes = 0, n_prims = 0, n_primary = 0;
-    // Persistent workgroups: the grid is the resident block count; block
-    // tiles are dealt round-robin (spreads the costly image centre over all
-    // CUs), and the counters are flushed once per wave at the very end.
-    const uint32_t per_tile = kTiles ? (a.tile_size / bw) * (a.tile_size / bh) : 0u;
-    const uint32_t bx_n = (a.W + bw - 1) / bw;
-    const uint32_t n_bt = kTiles ? a.n_tiles * per_tile : bx_n * ((a.H + bh - 1) / bh);
-    for (uint32_t bt = blockIdx.x; bt < n_bt; bt += gridDim.x) {
-        uint32_t x, y, k = 0, lx = 0, ly = 0;
+    const uint32_t per_tile = kTiles ? (a.tile_size / kTileSide) * (a.tile_size / kTileSide) : 0u;
+    const uint32_t bx_n = (a.W + kTileSide - 1) / kTileSide;
+    const uint32_t n_bt = kTiles ? a.n_tiles * per_tile : bx_n * ((a.H + kTileSide - 1) / kTileSide);
+    for (;;) {
+        __syncthreads();  // every wave is done with the previous tile_slot
+        if (threadIdx.x == 0)
+            tile_slot = static_cast<uint32_t>(atomicAdd(a.counters + kQueueSlot, 1ull));
+        __syncthreads();
+        const uint32_t bt = tile_slot;
+        if (bt >= n_bt) break;
+        uint32_t ox, oy, k = 0, olx = 0, oly = 0;  // block-tile origin (frame / packed tile)
         if (kTiles) {
-            const uint32_t tpr = a.tile_size / bw;
+            const uint32_t tpr = a.tile_size / kTileSide;
             k = bt / per_tile;
             const uint32_t b = bt - k * per_tile;
-            lx = (b % tpr) * bw + qx;
-            ly = (b / tpr) * bh + qy;
+            olx = (b % tpr) * kTileSide;
+            oly = (b / tpr) * kTileSide;
             const uint32_t tile = a.tiles[k];
-            x = (tile % a.tiles_x) * a.tile_size + lx;
-            y = (tile / a.tiles_x) * a.tile_size + ly;
+            ox = (tile % a.tiles_x) * a.tile_size + olx;
+            oy = (tile / a.tiles_x) * a.tile_size + oly;
         } else {
-            x = (bt % bx_n) * bw + qx;
-            y = (bt / bx_n) * bh + qy;
+            ox = (bt % bx_n) * kTileSide;
+            oy = (bt / bx_n) * kTileSide;
         }
-        const bool lane_pix = pix < a.ppw && x < a.W && y < a.H;
-        const bool leader = lane_pix && sub == 0;
-        const uint32_t pid = y * a.W + x;
-        const uint32_t hp = mix32(a.seedmix ^ pid);
-        float ar = 0.0f, ag = 0.0f, ab = 0.0f;
-        for (uint32_t r = 0; r < a.rounds; ++r) {
-            const uint32_t s = r * spw + sub;
-            const bool valid = lane_pix && s < a.spp;
-            n_primary += valid ? 1u : 0u;
-            const PixelOut c =
-                sample_color<kVar>(a, x, y, hp, s, valid, n_shadow, n_nodes, n_prims, stk);
-            col[threadIdx.x] = make_float4(c.r, c.g, c.b, 0.0f);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (leader) {
-                const uint32_t nv = min(spw, a.spp - r * spw);
-                const float4* src = col + threadIdx.x;  // this pixel's samples, in order
-                for (uint32_t j = 0; j < nv; ++j) {
-                    const float4 q = src[j];
-                    ar += q.x;
-                    ag += q.y;
-                    ab += q.z;
+        for (uint32_t wt = wave; wt < wtiles; wt += kBlockThreads / 64) {
+            const uint32_t qx = (wt % wtx) * tw + pix % tw;
+            const uint32_t qy = (wt / wtx) * th + pix / tw;
+            const uint32_t x = ox + qx, y = oy + qy;
+            const bool lane_pix = pix < a.ppw && x < a.W && y < a.H;
+            const bool leader = lane_pix && sub == 0;
+            const uint32_t pid = y * a.W + x;
+            const uint32_t hp = mix32(a.seedmix ^ pid);
+            for (uint32_t r = 0; r < a.rounds; ++r) {
+                const uint32_t s = r * spw + sub;
+                const bool valid = lane_pix && s < a.spp;
+                n_primary += valid ? 1u : 0u;
+                const PixelOut c =
+                    kVar == kVariantLaneUnified
+                        ? sample_color_unified<kChunk, kStats>(a, x, y, hp, s, valid, n_shadow,
+                                                               n_nodes, n_prims, stk)
+                        : sample_color<kVar, kChunk, kUni>(a, x, y, hp, s, valid, n_shadow, n_nodes,
+                                                           n_prims, stk);
+                col[threadIdx.x] = make_float4(c.r, c.g, c.b, 0.0f);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (leader) {
+                    // running sum lives in LDS (not in registers across the walks)
+                    float ar = 0.0f, ag = 0.0f, ab = 0.0f;
+                    if (r) {
+                        const float4 A = acc[threadIdx.x];
+                        ar = A.x;
+                        ag = A.y;
+                        ab = A.z;
+                    }
+                    const uint32_t nv = min(spw, a.spp - r * spw);
+                    const float4* src = col + threadIdx.x;  // this pixel's samples, in order
+                    for (uint32_t j = 0; j < nv; ++j) {
+                        const float4 q = src[j];
+                        ar += q.x;
+                        ag += q.y;
+                        ab += q.z;
+                    }
+                    acc[threadIdx.x] = make_float4(ar, ag, ab, 0.0f);
                 }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        if (leader) {
-            const PixelOut p{ar * a.inv_spp, ag * a.inv_spp, ab * a.inv_spp};
-            const uint32_t rgba = pack_rgba8(p);
-            if (kTiles) {
-                a.out8[(size_t)k * a.tile_size * a.tile_size + ly * a.tile_size + lx] = rgba;
-            } else {
-                a.out8[(size_t)y * a.W + x] = rgba;
-                if (a.out32) a.out32[(size_t)y * a.W + x] = make_float4(p.r, p.g, p.b, 1.0f);
+            if (leader) {
+                const float4 A = acc[threadIdx.x];
+                const PixelOut p{A.x * a.inv_spp, A.y * a.inv_spp, A.z * a.inv_spp};
+                const uint32_t rgba = pack_rgba8(p);
+                if (kTiles) {
+                    a.out8[(size_t)k * a.tile_size * a.tile_size + (oly + qy) * a.tile_size + olx + qx] =
+                        rgba;
+                } else {
+                    a.out8[(size_t)y * a.W + x] = rgba;
+                    if (a.out32) a.out32[(size_t)y * a.W + x] = make_float4(p.r, p.g, p.b, 1.0f);
+                }
+            } else if (kTiles && sub == 0 && pix < a.ppw) {
+                a.out8[(size_t)k * a.tile_size * a.tile_size + (oly + qy) * a.tile_size + olx + qx] =
+                    0u;  // off-image pixel of an edge tile
             }
-        } else if (kTiles && sub == 0 && pix < a.ppw) {
-            a.out8[(size_t)k * a.tile_size * a.tile_size + ly * a.tile_size + lx] = 0u;  // off-image
         }
     }
     flush_counters(a, n_primary, n_shadow, n_nodes, n_prims);
@@ -682,41 +836,92 @@ hipError_t launch_compat(const FrameArgs& a, hipStream_t st) {
 }
 
 size_t scene_lds_bytes(const FrameArgs& a) {
-    const size_t colours = kBlockThreads * sizeof(float4);
+    const size_t colours = 2 * kBlockThreads * sizeof(float4);  // sample colours + pixel sums
     if (a.variant == kVariantPacket)
         return colours + static_cast<size_t>(a.stack_entries) * (kBlockThreads / 64) * sizeof(PStackEntry);
     const uint32_t levels = a.sc.max_depth > 1 ? a.sc.max_depth - 1 : 1;
     return colours + static_cast<size_t>(levels) * kBlockThreads * sizeof(uint2);
 }
 
-// Resident workgroups per CU for a kernel at a given LDS size (queried once).
+// Resident workgroups on the device for a kernel at a given LDS size.  The
+// occupancy query is a host call: cache it per (kernel, LDS bytes, device) so
+// the launch path stays a single hipLaunchKernelGGL.
 template <typename K>
 static uint32_t resident_blocks(K kernel, size_t lds) {
-    static thread_local int dev_cached = -1, cus = 0;
+    struct Key {
+        const void* k;
+        size_t lds;
+        int dev;
+    };
+    static std::mutex mu;
+    static std::vector<std::pair<Key, uint32_t>> cache;
     int dev = 0;
     (void)hipGetDevice(&dev);
-    if (dev != dev_cached) {
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
-        dev_cached = dev;
+    const void* kp = reinterpret_cast<const void*>(kernel);
+    {
+        std::lock_guard<std::mutex> g(mu);
+        for (const auto& e : cache)
+            if (e.first.k == kp && e.first.lds == lds && e.first.dev == dev) return e.second;
     }
+    hipDeviceProp_t prop;
+    int cus = 256;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlockThreads, lds) != hipSuccess ||
         per_cu <= 0)
         per_cu = 4;
-    return static_cast<uint32_t>((cus > 0 ? cus : 256) * per_cu);
+    const uint32_t n = static_cast<uint32_t>(cus * per_cu);
+    std::lock_guard<std::mutex> g(mu);
+    cache.push_back({{kp, lds, dev}, n});
+    return n;
+}
+
+template <typename K>
+static void launch_persistent(K kernel, const FrameArgs& a, uint32_t n_bt, size_t lds,
+                              hipStream_t st) {
+    const uint32_t grid = std::min(n_bt, resident_blocks(kernel, lds));
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlockThreads), lds, st, a);
 }
 
 template <bool kTiles>
 static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStream_t st) {
-    if (a.variant == kVariantPacket) {
-        auto k = scene_kernel<kTiles, kVariantPacket>;
-        const uint32_t grid = std::min(n_bt, resident_blocks(k, lds));
-        hipLaunchKernelGGL(k, dim3(grid), dim3(kBlockThreads), lds, st, a);
-    } else {
-        auto k = scene_kernel<kTiles, kVariantLane>;
-        const uint32_t grid = std::min(n_bt, resident_blocks(k, lds));
-        hipLaunchKernelGGL(k, dim3(grid), dim3(kBlockThreads), lds, st, a);
+    if (a.variant == kVariantLaneUnified1) {  // default: counters only in stats frames
+        if (a.count_work)
+            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 1, false, true>, a, n_bt,
+                              lds, st);
+        else
+            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 1, false, false>, a, n_bt,
+                              lds, st);
+        return;
+    }
+    switch (a.variant) {
+        case kVariantPacket:
+            launch_persistent(scene_kernel<kTiles, kVariantPacket, 1, 4, false>, a, n_bt, lds, st);
+            break;
+        case kVariantLaneChunk2:
+            launch_persistent(scene_kernel<kTiles, kVariantLane, 1, 2, false>, a, n_bt, lds, st);
+            break;
+        case kVariantLaneUni1:
+            launch_persistent(scene_kernel<kTiles, kVariantLane, 1, 1, true>, a, n_bt, lds, st);
+            break;
+        case kVariantLaneUnified:
+            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false>, a, n_bt, lds, st);
+            break;
+        case kVariantLaneUnified1Stats:  // A/B only: variant 8 with the work counters compiled in
+            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 1, false, true>, a, n_bt,
+                              lds, st);
+            break;
+        case kVariantLaneUnified2NoStats:  // A/B only: variant 7 without the work counters
+            if (a.count_work)
+                launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true>, a, n_bt,
+                                  lds, st);
+            else
+                launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false>, a,
+                                  n_bt, lds, st);
+            break;
+        default:
+            launch_persistent(scene_kernel<kTiles, kVariantLane, 1, 4, false>, a, n_bt, lds, st);
+            break;
     }
 }
 
@@ -734,12 +939,12 @@ hipError_t launch_scene(const FrameArgs& a_in, hipStream_t st) {
     a.rounds = (a.spp + a.spw - 1) / a.spw;
     a.stack_entries = 8u * a.sc.max_depth + 8u;
     const size_t lds = scene_lds_bytes(a);
-    const uint32_t bw = 2u * a.tw, bh = 2u * a.th;
     if (a.tiles) {
-        const uint32_t per = (a.tile_size / bw) * (a.tile_size / bh);
+        const uint32_t per = (a.tile_size / kTileSide) * (a.tile_size / kTileSide);
         launch_scene_t<true>(a, a.n_tiles * per, lds, st);
     } else {
-        launch_scene_t<false>(a, ((a.W + bw - 1) / bw) * ((a.H + bh - 1) / bh), lds, st);
+        launch_scene_t<false>(a, ((a.W + kTileSide - 1) / kTileSide) * ((a.H + kTileSide - 1) / kTileSide),
+                              lds, st);
     }
     return hipGetLastError();
 }

@@ -9,7 +9,7 @@
 namespace rtamd {
 
 constexpr int kBlockThreads = 256;  // 4 waves of 64
-constexpr int kTileSide = 16;       // scene kernel: 16x16 pixels per workgroup, 8x8 per wave
+constexpr int kTileSide = 16;       // scene kernel: 16x16-pixel block tiles per workgroup
 constexpr uint32_t kMaxDepth = 16;  // octree depth limit (grid coordinates stay < 2^16, exact in f32)
 constexpr float kShadowEps = 1e-5f; // shadow-ray origin offset along the normal (world units)
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
@@ -17,7 +17,17 @@ constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 // scene kernel variants (rt_config.flags bits 16..19, RT_FLAG_VARIANT_SHIFT)
 constexpr uint32_t kVariantLane = 1;    // one ray per lane, per-thread LDS ancestor stack
 constexpr uint32_t kVariantPacket = 2;  // 64-ray wave packet, per-wave LDS stack, ballot masks
-constexpr uint32_t kVariantDefault = kVariantLane;
+constexpr uint32_t kVariantLaneChunk2 = 3;  // lane walk, 2 leaf spheres in flight (fewer VGPRs)
+constexpr uint32_t kVariantLaneUni1 = 4;    // lane walk + wave-uniform scalar leaf/node path, 1 in flight
+constexpr uint32_t kVariantLaneUnified = 7;   // one walk instance for primary + shadow, 2 in flight
+constexpr uint32_t kVariantLaneUnified1 = 8;  // same, 1 in flight; counters only in stats frames
+constexpr uint32_t kVariantLaneUnified1Stats = 9;    // A/B: 8 with counters always compiled in
+constexpr uint32_t kVariantLaneUnified2NoStats = 10; // A/B: 7 with counters only in stats frames
+
+// counters[] layout: [0..3] stats, [kQueueSlot] tile queue head (own cache line)
+constexpr uint32_t kQueueSlot = 8;
+constexpr uint32_t kCounterWords = 16;
+constexpr uint32_t kVariantDefault = 7;  // kVariantLaneUnified: best across C2/C3/C5 (tools/variants.py)
 
 // Pinhole camera (include/camera.h:9-56): K and R column-major like glm.
 struct CamArgs {
@@ -72,6 +82,7 @@ struct FrameArgs {
     uint32_t stack_entries;  // packet kernel: LDS stack entries per wave
     // wave mapping (set by launch_scene): a wave = ppw pixels (tw x th) x spw samples
     uint32_t spw, ppw, tw, th, rounds;
+    uint32_t count_work;  // 1: also count node visits / sphere tests (stats frames)
 };
 
 }  // namespace rtamd

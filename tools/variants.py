@@ -4,8 +4,8 @@
     python tools/variants.py [--configs c2,c3] [--variants 1,2] [--rounds 3]
 
 For each config, one renderer per variant renders the same frame; rounds are
-interleaved (v1, v2, v1, v2, ...) and the kernel time (hipEvent, rt_stats.ms)
-is reported as median/min.  Every variant's image must equal variant 1's
+interleaved (v1, v2, v1, v2, ...) and the kernel time (HIP events around
+plain, counter-free frames) is reported as median/min.  Every variant's image must equal variant 1's
 byte for byte (results are variant-independent by construction).
 """
 from __future__ import annotations
@@ -45,13 +45,20 @@ def main():
             r.set_scene(sp, al, max_depth=cfg.max_depth)
             r.render(stats=True)  # warm-up
             rs[v] = r
+        # timed frames are plain frames (no work counters), HIP events on a torch stream
+        import torch
+        stream = torch.cuda.Stream()
         times = {v: [] for v in variants}
-        stats = {}
+        stats = {v: rs[v].render(stats=True) for v in variants}
         for _ in range(args.rounds):
             for v in variants:
-                st = rs[v].render(stats=True)
-                times[v].append(st.ms)
-                stats[v] = st
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                rs[v].render(None, stream.cuda_stream)
+                e1.record(stream)
+                e1.synchronize()
+                times[v].append(e0.elapsed_time(e1))
         ref = rs[variants[0]].readback()
         res = {}
         for v in variants:
