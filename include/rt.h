@@ -79,7 +79,9 @@ enum {
     RT_FLAG_NO_SHADOWS = 1u << 3,  /* skip shadow rays (Lambert without visibility) */
     /* bits 16..19: scene-kernel variant for A/B runs (0 = default = 1, one ray
      * per lane; 2 = 64-ray wave packets); images are identical */
-    RT_FLAG_VARIANT_SHIFT = 16
+    RT_FLAG_VARIANT_SHIFT = 16,
+    /* bits 20..23: A/B toggles that switch single optimisations off (0 = all on) */
+    RT_FLAG_OPT_SHIFT = 20
 };
 
 typedef struct rt_config {

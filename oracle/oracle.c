@@ -566,6 +566,15 @@ int orc_trace_brute(const orc_scene* s, const float o[3], const float d[3], floa
 
 #define SHADOW_EPS 1e-5f
 
+/* Pairwise sum of n (a power of two) values: T(lo, n) = T(lo, n/2) + T(lo+n/2, n/2).
+ * This is exactly what a shfl_xor butterfly over n lanes produces (each step
+ * adds the same two partial sums in every lane; float + is commutative). */
+static float tree_sum(const float* v, uint32_t n) {
+    if (n == 1) return v[0];
+    const uint32_t h = n / 2;
+    return tree_sum(v, h) + tree_sum(v + h, h);
+}
+
 void orc_render_scene(const orc_scene* s, uint32_t W, uint32_t H, const float pose[16],
                       const float K[9], uint32_t spp, uint32_t seed, uint32_t flags,
                       const float light_dir[3], float ambient, uint32_t x0, uint32_t y0,
@@ -598,6 +607,14 @@ void orc_render_scene(const orc_scene* s, uint32_t W, uint32_t H, const float po
         for (uint32_t x = x0; x < x1; ++x) {
             const uint32_t pid = y * W + x;
             const uint32_t hp = mix32(seedmix ^ pid);
+            /* Per-pixel sum (DESIGN.md "Accumulate"): samples go in rounds of
+             * spw = min(spp, 64); each round is pairwise-summed over g =
+             * pow2ceil(spw) slots (missing samples are 0) and the round sums
+             * are added in order: acc = T0, acc = acc + T1, ... */
+            const uint32_t spw = spp >= 64u ? 64u : spp;
+            uint32_t g = 1;
+            while (g < spw) g *= 2;
+            float rbuf[3][64];
             float ar = 0.0f, ag = 0.0f, ab = 0.0f;
             for (uint32_t sidx = 0; sidx < spp; ++sidx) {
                 float u = (float)x, v = (float)y;
@@ -641,9 +658,25 @@ void orc_render_scene(const orc_scene* s, uint32_t W, uint32_t H, const float po
                 }
                 c2 += nn;
                 c3 += pp;
-                ar += cr;
-                ag += cg;
-                ab += cb;
+                const uint32_t slot = sidx % spw;
+                if (slot == 0)
+                    for (uint32_t q = 0; q < g; ++q) rbuf[0][q] = rbuf[1][q] = rbuf[2][q] = 0.0f;
+                rbuf[0][slot] = cr;
+                rbuf[1][slot] = cg;
+                rbuf[2][slot] = cb;
+                if (slot == spw - 1 || sidx == spp - 1) {
+                    const float tr = tree_sum(rbuf[0], g), tg = tree_sum(rbuf[1], g),
+                                tb = tree_sum(rbuf[2], g);
+                    if (sidx < spw) {
+                        ar = tr;
+                        ag = tg;
+                        ab = tb;
+                    } else {
+                        ar = ar + tr;
+                        ag = ag + tg;
+                        ab = ab + tb;
+                    }
+                }
             }
             const float mr = ar * inv_spp, mg = ag * inv_spp, mb = ab * inv_spp;
             uint8_t* px = out8 + 4u * (size_t)pid;

@@ -29,6 +29,7 @@ RT_FLAG_NO_JITTER = 1 << 1
 RT_FLAG_RADIANCE = 1 << 2
 RT_FLAG_NO_SHADOWS = 1 << 3
 RT_FLAG_VARIANT_SHIFT = 16
+RT_FLAG_OPT_SHIFT = 20
 VARIANT_LANE = 1    # one ray per lane
 VARIANT_PACKET = 2  # 64-ray wave packets (default)
 

@@ -137,8 +137,11 @@ void fill_frame_args(rt_renderer* r, FrameArgs& a) {
     a.ambient = r->cfg.ambient;
     a.inv_spp = 1.0f / static_cast<float>(a.spp);
     a.counters = r->counters.p;
+    a.sc.opt = (r->cfg.flags >> RT_FLAG_OPT_SHIFT) & 0xFu;
     const uint32_t v = (r->cfg.flags >> RT_FLAG_VARIANT_SHIFT) & 0xFu;
-    a.variant = v ? v : kVariantDefault;
+    // default: the counter-free unified walk for multi-sample frames, the
+    // counting one for 1-spp frames (faster there, tools/variants.py A/B)
+    a.variant = v ? v : (a.spp >= 8u ? kVariantLaneUnified2NoStats : kVariantLaneUnified);
 }
 
 int upload_scene(rt_renderer* r) {

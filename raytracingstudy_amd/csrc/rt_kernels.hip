@@ -298,7 +298,8 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             c0 >>= m;
             c1 >>= m;
             c2 >>= m;
-            node = depth ? stk[(depth - 1) * kBlockThreads] : S.root;
+            // m == 1: the ancestor is the node we are iterating (still in `node`)
+            if (m > 1 || (S.opt & kOptNoParentReuse)) node = depth ? stk[(depth - 1) * kBlockThreads] : S.root;
             t = texit;
         }
     }
@@ -698,17 +699,16 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
 template <bool kTiles, uint32_t kVar, int kMinW, int kChunk, bool kUni, bool kStats = true>
 __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
-    float4* col = lds;                  // [256] sample colours
-    float4* acc = lds + kBlockThreads;  // [256] running pixel sums (leader lanes' slots)
+    float4* acc = lds;  // [256] running pixel sums (leader lanes' slots)
     __shared__ uint32_t tile_slot;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     void* stk;
     if (kVar == kVariantPacket)
-        stk = reinterpret_cast<PStackEntry*>(lds + 2 * kBlockThreads) + wave * a.stack_entries;
+        stk = reinterpret_cast<PStackEntry*>(lds + kBlockThreads) + wave * a.stack_entries;
     else
-        stk = reinterpret_cast<uint2*>(lds + 2 * kBlockThreads) + threadIdx.x;
-    const uint32_t spw = a.spw, tw = a.tw, th = a.th;
-    const uint32_t pix = lane / spw, sub = lane - pix * spw;
+        stk = reinterpret_cast<uint2*>(lds + kBlockThreads) + threadIdx.x;
+    const uint32_t spw = a.spw, g = a.g, tw = a.tw, th = a.th;
+    const uint32_t pix = lane / g, sub = lane & (g - 1u);
     const uint32_t wtx = kTileSide / tw, wtiles = wtx * (kTileSide / th);
     uint32_t n_shadow = 0, n_nodes = 0, n_prims = 0, n_primary = 0;
     const uint32_t per_tile = kTiles ? (a.tile_size / kTileSide) * (a.tile_size / kTileSide) : 0u;
@@ -745,40 +745,32 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
             const uint32_t hp = mix32(a.seedmix ^ pid);
             for (uint32_t r = 0; r < a.rounds; ++r) {
                 const uint32_t s = r * spw + sub;
-                const bool valid = lane_pix && s < a.spp;
+                const bool valid = lane_pix && sub < spw && s < a.spp;
                 n_primary += valid ? 1u : 0u;
-                const PixelOut c =
+                PixelOut c =
                     kVar == kVariantLaneUnified
                         ? sample_color_unified<kChunk, kStats>(a, x, y, hp, s, valid, n_shadow,
                                                                n_nodes, n_prims, stk)
                         : sample_color<kVar, kChunk, kUni>(a, x, y, hp, s, valid, n_shadow, n_nodes,
                                                            n_prims, stk);
-                col[threadIdx.x] = make_float4(c.r, c.g, c.b, 0.0f);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                // Pixel sum of this round: pairwise butterfly over the pixel's g
+                // lanes (missing samples are 0) = oracle.c:tree_sum; rounds are
+                // then added in order in the leader's LDS slot.
+                if (!valid) c = PixelOut{0.0f, 0.0f, 0.0f};
+                for (uint32_t k = 1; k < g; k <<= 1) {
+                    c.r += __shfl_xor(c.r, static_cast<int>(k), 64);
+                    c.g += __shfl_xor(c.g, static_cast<int>(k), 64);
+                    c.b += __shfl_xor(c.b, static_cast<int>(k), 64);
+                }
                 if (leader) {
-                    // running sum lives in LDS (not in registers across the walks)
-                    float ar = 0.0f, ag = 0.0f, ab = 0.0f;
                     if (r) {
                         const float4 A = acc[threadIdx.x];
-                        ar = A.x;
-                        ag = A.y;
-                        ab = A.z;
+                        c.r = A.x + c.r;
+                        c.g = A.y + c.g;
+                        c.b = A.z + c.b;
                     }
-                    const uint32_t nv = min(spw, a.spp - r * spw);
-                    const float4* src = col + threadIdx.x;  // this pixel's samples, in order
-                    for (uint32_t j = 0; j < nv; ++j) {
-                        const float4 q = src[j];
-                        ar += q.x;
-                        ag += q.y;
-                        ab += q.z;
-                    }
-                    acc[threadIdx.x] = make_float4(ar, ag, ab, 0.0f);
+                    acc[threadIdx.x] = make_float4(c.r, c.g, c.b, 0.0f);
                 }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
             if (leader) {
                 const float4 A = acc[threadIdx.x];
@@ -836,7 +828,7 @@ hipError_t launch_compat(const FrameArgs& a, hipStream_t st) {
 }
 
 size_t scene_lds_bytes(const FrameArgs& a) {
-    const size_t colours = 2 * kBlockThreads * sizeof(float4);  // sample colours + pixel sums
+    const size_t colours = kBlockThreads * sizeof(float4);  // pixel sums
     if (a.variant == kVariantPacket)
         return colours + static_cast<size_t>(a.stack_entries) * (kBlockThreads / 64) * sizeof(PStackEntry);
     const uint32_t levels = a.sc.max_depth > 1 ? a.sc.max_depth - 1 : 1;
@@ -929,8 +921,9 @@ hipError_t launch_scene(const FrameArgs& a_in, hipStream_t st) {
     FrameArgs a = a_in;
     // wave mapping: spw samples x ppw pixels per wave (see scene_kernel)
     a.spw = a.spp >= 64u ? 64u : a.spp;
-    uint32_t ppw = 1;
-    while (ppw * 2u * a.spw <= 64u) ppw *= 2u;
+    a.g = 1;
+    while (a.g < a.spw) a.g *= 2u;  // lanes per pixel (butterfly width)
+    const uint32_t ppw = 64u / a.g;
     a.ppw = ppw;
     uint32_t lg = 0;
     while ((1u << lg) < ppw) ++lg;

@@ -24,10 +24,12 @@ constexpr uint32_t kVariantLaneUnified1 = 8;  // same, 1 in flight; counters onl
 constexpr uint32_t kVariantLaneUnified1Stats = 9;    // A/B: 8 with counters always compiled in
 constexpr uint32_t kVariantLaneUnified2NoStats = 10; // A/B: 7 with counters only in stats frames
 
+// A/B toggles (rt_config.flags bits 20..23), results identical either way
+constexpr uint32_t kOptNoParentReuse = 1;  // always re-read the ancestor from the LDS stack
+
 // counters[] layout: [0..3] stats, [kQueueSlot] tile queue head (own cache line)
 constexpr uint32_t kQueueSlot = 8;
 constexpr uint32_t kCounterWords = 16;
-constexpr uint32_t kVariantDefault = 7;  // kVariantLaneUnified: best across C2/C3/C5 (tools/variants.py)
 
 // Pinhole camera (include/camera.h:9-56): K and R column-major like glm.
 struct CamArgs {
@@ -56,6 +58,7 @@ struct SceneArgs {
     float rmin[3];
     float scale[3];          // G / (rmax - rmin), f32
     float G;
+    uint32_t opt;            // kOpt* toggles (A/B only; 0 = all optimisations on)
 };
 
 struct FrameArgs {
@@ -81,7 +84,7 @@ struct FrameArgs {
     uint32_t variant;   // scene kernel variant (kVariant*)
     uint32_t stack_entries;  // packet kernel: LDS stack entries per wave
     // wave mapping (set by launch_scene): a wave = ppw pixels (tw x th) x spw samples
-    uint32_t spw, ppw, tw, th, rounds;
+    uint32_t spw, g, ppw, tw, th, rounds;  // g = pow2ceil(spw) lanes per pixel
     uint32_t count_work;  // 1: also count node visits / sphere tests (stats frames)
 };
 

@@ -71,7 +71,7 @@ class KernelRenderer:
                  seed: int = 0x2545F491, device: int = -1, jitter: Optional[bool] = None,
                  shadows: bool = True, radiance: bool = False,
                  light_dir: Sequence[float] = (1.0, 1.0, -1.0), ambient: float = 0.1,
-                 variant: int = 0):
+                 variant: int = 0, opt_off: int = 0):
         lib = _lib.load()
         cfg = RtConfig()
         lib.rt_config_default(ctypes.byref(cfg))
@@ -90,6 +90,7 @@ class KernelRenderer:
         if radiance:
             flags |= RT_FLAG_RADIANCE
         flags |= (int(variant) & 0xF) << _lib.RT_FLAG_VARIANT_SHIFT
+        flags |= (int(opt_off) & 0xF) << _lib.RT_FLAG_OPT_SHIFT
         cfg.flags = flags
         for i in range(3):
             cfg.light_dir[i] = float(light_dir[i])

@@ -31,7 +31,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--spp", type=int, default=0, help="override spp")
     args = ap.parse_args()
-    variants = [int(v) for v in args.variants.split(",")]
+    # a variant spec is "V" or "V:OPT" (OPT = rt_config opt-off bits, A/B toggles)
+    variants = args.variants.split(",")
     out = {}
     for name in args.configs.split(","):
         cfg = rt.CONFIGS[name]
@@ -39,7 +40,9 @@ def main():
         sp, al = rt.generate_spheres(cfg.n_spheres, rt.SEED)
         rs = {}
         for v in variants:
-            r = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=spp, variant=v)
+            vv, _, oo = v.partition(":")
+            r = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=spp, variant=int(vv),
+                                  opt_off=int(oo or 0))
             r.resize(cfg.width, cfg.height)
             r.setPosition(scene_pose())
             r.set_scene(sp, al, max_depth=cfg.max_depth)
@@ -70,11 +73,11 @@ def main():
                       "Mrays_s": round(rays / med / 1e3, 1), "rays": int(rays),
                       "nodes_per_ray": round(st.nodes_visited / rays, 2),
                       "prims_per_ray": round(st.prims_tested / rays, 2),
-                      "image_equal_to_v%d" % variants[0]: bool(np.array_equal(img, ref))}
+                      "image_equal_to_v%s" % variants[0]: bool(np.array_equal(img, ref))}
             rs[v].close()
         out[f"{name} spp{spp}"] = res
         print(name, json.dumps(res), flush=True)
-    return 0 if all(r[v]["image_equal_to_v%d" % variants[0]] for r in out.values() for v in r) else 1
+    return 0 if all(r[v]["image_equal_to_v%s" % variants[0]] for r in out.values() for v in r) else 1
 
 
 if __name__ == "__main__":
