@@ -217,6 +217,10 @@ def main():
                 "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "alg_bytes_per_launch": int(alg_bytes),
+                "note": ("algorithmic bytes = SURVEY 8d D4 node+sphere records touched per ray + "
+                         "framebuffer; the octree is cache-resident (L1/L2/MALL), so HBM sees only "
+                         "`traffic` bytes per launch (PMC, corrected)"),
+                "hbm_traffic_gbs": (round(traffic / (kern_ms / 1e3) / 1e9, 3) if traffic else None),
                 "per_ray": {"nodes": float(cnt[2].item()) / float(cnt[0].item() + cnt[1].item()),
                             "prims": float(cnt[3].item()) / float(cnt[0].item() + cnt[1].item())},
             },

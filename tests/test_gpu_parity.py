@@ -91,14 +91,16 @@ def _scene_pair(oracle, n, w, h, spp, depth=7, pose=None, shadows=True, jitter=N
     return img, rad, st, info, ref8, ref32, cnt, oinfo
 
 
-VARIANTS = [rt._lib.VARIANT_LANE, rt._lib.VARIANT_PACKET]
+# 0 = the library default; 1 lane walk; 2 wave packets; 3 lane walk, 2 spheres in
+# flight; 7 unified primary+shadow walk; 10 unified, counters only in stats frames
+VARIANTS = [0, rt._lib.VARIANT_LANE, rt._lib.VARIANT_PACKET, 3, 7, 10]
 
 
 def _check_counts(st, cnt, variant):
     # rays cast are a property of the image; node/prim counts are the work of
-    # the traversal: the one-ray-per-lane walk reproduces the oracle's exactly
+    # the traversal: every one-ray-per-lane walk reproduces the oracle's exactly
     assert (st.primary_rays, st.shadow_rays) == (int(cnt[0]), int(cnt[1]))
-    if variant == rt._lib.VARIANT_LANE:
+    if variant != rt._lib.VARIANT_PACKET:
         assert (st.nodes_visited, st.prims_tested) == (int(cnt[2]), int(cnt[3]))
 
 
