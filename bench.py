@@ -42,6 +42,12 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU-baseline sample duration")
     ap.add_argument("--variant", type=int, default=0, help="scene-kernel variant (0 = default)")
+    ap.add_argument("--shard", default="",
+                    help="R/N: render only rank R's tiles of an N-way split on this one GPU "
+                         "(projects the per-GPU kernel time of an N-GPU run; no gather)")
+    ap.add_argument("--tiles", action="store_true",
+                    help="use the multi-GPU tile path (render_tiles + gather + unpack) even at N=1, "
+                         "and check the frame against a whole-frame render")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="PMC traffic summary written by tools/pmc_traffic.py")
     return ap.parse_args()
@@ -87,7 +93,7 @@ def main():
 
     import raytracingstudy_amd as rt
     from raytracingstudy_amd.camera import scene_pose
-    from raytracingstudy_amd import tiles as T
+    from raytracingstudy_amd.dist import TileSharder
 
     torch.cuda.set_device(local)
     if world > 1:
@@ -114,12 +120,18 @@ def main():
     assert sptr, "need a non-null HIP stream handle"
     W, H, ts = cfg.width, cfg.height, rt.configs.TILE_SIZE
     frame = torch.empty(W * H * 4, dtype=torch.uint8, device=dev)
-    if world > 1:
-        my_ids = T.tiles_for_rank(W, H, rank, world, ts)
-        slab = T.slab_tiles(W, H, world, ts)
-        packed = torch.zeros(slab * ts * ts * 4, dtype=torch.uint8, device=dev)
-        all_ids = [T.tiles_for_rank(W, H, k, world, ts) for k in range(world)]
-        gathered = [torch.empty_like(packed) for _ in range(world)] if rank == 0 else None
+    tiled = world > 1 or args.tiles or bool(args.shard)
+    if tiled:
+        # tests/test_tiles_dist.py drives the same TileSharder with gloo on CPU
+        if args.shard:
+            sr, sn = (int(v) for v in args.shard.split("/"))
+            sharder = TileSharder(W, H, sr, sn, ts)
+            sharder.world = 1  # local projection: no gather, this GPU renders rank sr's tiles
+            sharder.rank = 0
+        else:
+            sharder = TileSharder(W, H, rank, world, ts)
+        my_ids = sharder.ids
+        packed = sharder.new_slab(torch, device=dev)
 
     events = []
 
@@ -128,21 +140,20 @@ def main():
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        if world == 1:
+        if not tiled:
             r.render(frame.data_ptr(), sptr)
         else:
             r.render_tiles(my_ids, ts, packed.data_ptr(), sptr)
         if record:
             e1.record(stream)
             events.append((e0, e1))
-        if world > 1:
-            dist.gather(packed, gathered, dst=0)
-            if rank == 0:
-                for k in range(world):
-                    r.unpack_tiles(gathered[k].data_ptr(), all_ids[k], ts, frame.data_ptr(), sptr)
+        if tiled and not args.shard:
+            gathered = sharder.gather(packed)  # RCCL gather of the equal-size slabs to rank 0
+            sharder.unpack(gathered, lambda slab, ids: r.unpack_tiles(slab.data_ptr(), ids, ts,
+                                                                      frame.data_ptr(), sptr))
 
     # counted rays of one frame on this rank (deterministic; equal to the oracle's)
-    if world == 1:
+    if not tiled:
         st = r.render(frame.data_ptr(), sptr, stats=True)
     else:
         st = r.render_tiles(my_ids, ts, packed.data_ptr(), sptr, stats=True)
@@ -176,7 +187,7 @@ def main():
     if rank == 0:
         value = rays_frame * args.steps / elapsed / 1e6
         # roofline of the dominant kernel on this rank: algorithmic bytes per launch
-        pix = (W * H) if world == 1 else len(my_ids) * ts * ts
+        pix = (W * H) if not tiled else len(my_ids) * ts * ts
         alg_bytes = float(cnt[2].item()) * NODE_BYTES + float(cnt[3].item()) * PRIM_BYTES + pix * PIXEL_BYTES
         achieved = alg_bytes / (kern_ms / 1e3) / 1e9
         traffic = None
@@ -206,7 +217,7 @@ def main():
                 "width": W, "height": H, "spp": cfg.spp, "n_spheres": cfg.n_spheres,
                 "octree_depth": info["max_depth"], "octree_nodes": info["n_nodes"],
                 "prim_refs": info["n_prim_refs"], "leaf_capacity": rt.configs.LEAF_CAPACITY,
-                "parallelism": f"tiles{ts}x{world}" if world > 1 else "single",
+                "parallelism": f"tiles{ts}x{world}" if tiled else "single",
                 "rays_per_frame": int(rays_frame),
                 "primary_per_frame": int(tot[0].item()), "shadow_per_frame": int(tot[1].item()),
                 "kernel_ms": round(kern_ms, 4),
@@ -226,6 +237,15 @@ def main():
             },
             "cpu_baseline": None,
         }
+        if args.shard:
+            out["config"]["shard"] = args.shard
+            out["metric"] += f" [projection: rank {args.shard} tiles only]"
+        if tiled and not args.shard:
+            # the gathered frame must equal a whole-frame render, byte for byte
+            whole = torch.empty_like(frame)
+            r.render(whole.data_ptr(), sptr)
+            torch.cuda.synchronize(dev)
+            out["config"]["tiles_frame_check"] = bool(torch.equal(whole, frame))
         if world == 1 and args.cpu_baseline == "auto":
             try:
                 out["cpu_baseline"] = cpu_baseline(cfg, K, pose, args.cpu_seconds)

@@ -709,11 +709,12 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
         stk = reinterpret_cast<uint2*>(lds + kBlockThreads) + threadIdx.x;
     const uint32_t spw = a.spw, g = a.g, tw = a.tw, th = a.th;
     const uint32_t pix = lane / g, sub = lane & (g - 1u);
-    const uint32_t wtx = kTileSide / tw, wtiles = wtx * (kTileSide / th);
+    const uint32_t bts = a.bts;  // block-tile side (16, or 8/4 for small frames: launch_scene)
+    const uint32_t wtx = bts / tw, wtiles = wtx * (bts / th);
     uint32_t n_shadow = 0, n_nodes = 0, n_prims = 0, n_primary = 0;
-    const uint32_t per_tile = kTiles ? (a.tile_size / kTileSide) * (a.tile_size / kTileSide) : 0u;
-    const uint32_t bx_n = (a.W + kTileSide - 1) / kTileSide;
-    const uint32_t n_bt = kTiles ? a.n_tiles * per_tile : bx_n * ((a.H + kTileSide - 1) / kTileSide);
+    const uint32_t per_tile = kTiles ? (a.tile_size / bts) * (a.tile_size / bts) : 0u;
+    const uint32_t bx_n = (a.W + bts - 1) / bts;
+    const uint32_t n_bt = kTiles ? a.n_tiles * per_tile : bx_n * ((a.H + bts - 1) / bts);
     for (;;) {
         __syncthreads();  // every wave is done with the previous tile_slot
         if (threadIdx.x == 0)
@@ -723,17 +724,17 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
         if (bt >= n_bt) break;
         uint32_t ox, oy, k = 0, olx = 0, oly = 0;  // block-tile origin (frame / packed tile)
         if (kTiles) {
-            const uint32_t tpr = a.tile_size / kTileSide;
+            const uint32_t tpr = a.tile_size / bts;
             k = bt / per_tile;
             const uint32_t b = bt - k * per_tile;
-            olx = (b % tpr) * kTileSide;
-            oly = (b / tpr) * kTileSide;
+            olx = (b % tpr) * bts;
+            oly = (b / tpr) * bts;
             const uint32_t tile = a.tiles[k];
             ox = (tile % a.tiles_x) * a.tile_size + olx;
             oy = (tile / a.tiles_x) * a.tile_size + oly;
         } else {
-            ox = (bt % bx_n) * kTileSide;
-            oy = (bt / bx_n) * kTileSide;
+            ox = (bt % bx_n) * bts;
+            oy = (bt / bx_n) * bts;
         }
         for (uint32_t wt = wave; wt < wtiles; wt += kBlockThreads / 64) {
             const uint32_t qx = (wt % wtx) * tw + pix % tw;
@@ -868,10 +869,25 @@ static uint32_t resident_blocks(K kernel, size_t lds) {
     return n;
 }
 
+// Block tiles in the frame (or in the packed tile list) for block-tile side b.
+static uint32_t count_block_tiles(const FrameArgs& a, uint32_t b) {
+    if (a.tiles) return a.n_tiles * (a.tile_size / b) * (a.tile_size / b);
+    return ((a.W + b - 1) / b) * ((a.H + b - 1) / b);
+}
+
+// Persistent launch: grid = resident workgroups; the block-tile side shrinks
+// (16 -> 8 -> 4 pixels, never below two wave tiles) until the tile queue holds
+// >= 4 tiles per resident workgroup, so a small frame (one rank's share of a
+// multi-GPU frame) still keeps every CU busy to the end.
 template <typename K>
-static void launch_persistent(K kernel, const FrameArgs& a, uint32_t n_bt, size_t lds,
+static void launch_persistent(K kernel, const FrameArgs& a_in, uint32_t, size_t lds,
                               hipStream_t st) {
-    const uint32_t grid = std::min(n_bt, resident_blocks(kernel, lds));
+    FrameArgs a = a_in;
+    const uint32_t res = resident_blocks(kernel, lds);
+    const uint32_t min_side = 2u * std::max(a.tw, a.th);
+    a.bts = kTileSide;
+    while (a.bts / 2u >= min_side && count_block_tiles(a, a.bts) < 4u * res) a.bts /= 2u;
+    const uint32_t grid = std::min(count_block_tiles(a, a.bts), res);
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlockThreads), lds, st, a);
 }
 
@@ -932,13 +948,10 @@ hipError_t launch_scene(const FrameArgs& a_in, hipStream_t st) {
     a.rounds = (a.spp + a.spw - 1) / a.spw;
     a.stack_entries = 8u * a.sc.max_depth + 8u;
     const size_t lds = scene_lds_bytes(a);
-    if (a.tiles) {
-        const uint32_t per = (a.tile_size / kTileSide) * (a.tile_size / kTileSide);
-        launch_scene_t<true>(a, a.n_tiles * per, lds, st);
-    } else {
-        launch_scene_t<false>(a, ((a.W + kTileSide - 1) / kTileSide) * ((a.H + kTileSide - 1) / kTileSide),
-                              lds, st);
-    }
+    if (a.tiles)
+        launch_scene_t<true>(a, 0, lds, st);
+    else
+        launch_scene_t<false>(a, 0, lds, st);
     return hipGetLastError();
 }
 

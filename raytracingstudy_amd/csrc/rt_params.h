@@ -9,7 +9,7 @@
 namespace rtamd {
 
 constexpr int kBlockThreads = 256;  // 4 waves of 64
-constexpr int kTileSide = 16;       // scene kernel: 16x16-pixel block tiles per workgroup
+constexpr uint32_t kTileSide = 16;  // scene kernel: largest block tile (16x16 pixels per workgroup)
 constexpr uint32_t kMaxDepth = 16;  // octree depth limit (grid coordinates stay < 2^16, exact in f32)
 constexpr float kShadowEps = 1e-5f; // shadow-ray origin offset along the normal (world units)
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
@@ -86,6 +86,7 @@ struct FrameArgs {
     // wave mapping (set by launch_scene): a wave = ppw pixels (tw x th) x spw samples
     uint32_t spw, g, ppw, tw, th, rounds;  // g = pow2ceil(spw) lanes per pixel
     uint32_t count_work;  // 1: also count node visits / sphere tests (stats frames)
+    uint32_t bts;         // block-tile side in pixels (set by the launcher)
 };
 
 }  // namespace rtamd

@@ -40,12 +40,19 @@ class TileSharder:
         return torch_mod.zeros(self.slab_elems, dtype=dtype, device=device)
 
     def gather(self, slab, group=None):
-        """Equal-size gather of every rank's slab to rank 0; returns the list on rank 0."""
-        import torch
-        import torch.distributed as dist
-        out = [torch.empty_like(slab) for _ in range(self.world)] if self.rank == 0 else None
+        """Equal-size gather of every rank's slab to rank 0; returns the list on rank 0.
+        The receive buffers are allocated once and reused every frame."""
         if self.world == 1:
             return [slab]
+        import torch
+        import torch.distributed as dist
+        out = None
+        if self.rank == 0:
+            key = (tuple(slab.shape), slab.dtype, slab.device)
+            if getattr(self, "_recv_key", None) != key:
+                self._recv = [torch.empty_like(slab) for _ in range(self.world)]
+                self._recv_key = key
+            out = self._recv
         dist.gather(slab, out, dst=0, group=group)
         return out
 
