@@ -245,20 +245,24 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         if (leaf(S.root.x, S.root.y)) return true;
     } else {
         uint2 node = S.root;
-        uint32_t depth = 0, c0 = 0, c1 = 0, c2 = 0;
+        // Cell = (depth, lower corner l* in finest-grid units, size = G >> depth):
+        // mid plane = l + size/2, exit plane = l + size: the same integers (hence
+        // the same plane values) as the oracle's c * size forms, 3 VALU a plane.
+        uint32_t depth = 0, l0 = 0, l1 = 0, l2 = 0, size = G;
         float t = t0;
         // Hard cap (never reached by a correct walk: a ray crosses < 3*G cells
         // and each crossing costs at most one descent): no input can hang the GPU.
         for (uint32_t it = 0, cap = 8u * G + 64u; it < cap; ++it) {
-            const uint32_t hs = D - depth - 1u;  // log2 of the half cell size
-            uint32_t bits = 0;
-            if (plane(0, (2u * c0 + 1u) << hs) <= t) bits |= 1u;
-            if (plane(1, (2u * c1 + 1u) << hs) <= t) bits |= 2u;
-            if (plane(2, (2u * c2 + 1u) << hs) <= t) bits |= 4u;
+            const uint32_t half = size >> 1;
+            const bool b0 = plane(0, l0 + half) <= t;
+            const bool b1 = plane(1, l1 + half) <= t;
+            const bool b2 = plane(2, l2 + half) <= t;
+            const uint32_t bits = (b0 ? 1u : 0u) | (b1 ? 2u : 0u) | (b2 ? 4u : 0u);
             const uint32_t child = bits ^ mask;
-            c0 = 2u * c0 + (bits & 1u);
-            c1 = 2u * c1 + ((bits >> 1) & 1u);
-            c2 = 2u * c2 + (bits >> 2);
+            l0 += b0 ? half : 0u;
+            l1 += b1 ? half : 0u;
+            l2 += b2 ? half : 0u;
+            size = half;
             depth += 1;
             const uint32_t valid = node.y & 0xFFu;
             if (valid & (1u << child)) {
@@ -278,26 +282,28 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 }
                 if (leaf(rec.x, rec.y)) return true;
             }
-            const uint32_t ls = D - depth;  // log2 of the cell size
-            const float e0 = plane(0, (c0 + 1u) << ls);
-            const float e1 = plane(1, (c1 + 1u) << ls);
-            const float e2 = plane(2, (c2 + 1u) << ls);
+            const float e0 = plane(0, l0 + size);
+            const float e1 = plane(1, l1 + size);
+            const float e2 = plane(2, l2 + size);
             float texit = e0 < e1 ? e0 : e1;
             texit = texit < e2 ? texit : e2;
             if (!kAnyHit && best_t < texit) break;
             if (texit >= t1) break;
-            uint32_t diff = 0;
-            const uint32_t lim = 1u << depth;
-            bool out = false;
-            if (e0 == texit) { diff |= c0 ^ (c0 + 1u); c0 += 1u; out |= c0 >= lim; }
-            if (e1 == texit) { diff |= c1 ^ (c1 + 1u); c1 += 1u; out |= c1 >= lim; }
-            if (e2 == texit) { diff |= c2 ^ (c2 + 1u); c2 += 1u; out |= c2 >= lim; }
-            if (out) break;
-            const uint32_t m = 32u - __builtin_clz(diff);
+            // step every axis whose exit plane is texit; the flipped bits give the
+            // common ancestor (oracle.c: diff of the cell coordinates)
+            const uint32_t n0 = e0 == texit ? l0 + size : l0;
+            const uint32_t n1 = e1 == texit ? l1 + size : l1;
+            const uint32_t n2 = e2 == texit ? l2 + size : l2;
+            if ((n0 | n1 | n2) >= G) break;  // left the root
+            const uint32_t diff = (l0 ^ n0) | (l1 ^ n1) | (l2 ^ n2);
+            const uint32_t top = 31u - __builtin_clz(diff);  // highest flipped bit
+            // ancestor cell size = 2^(top+1); its depth = D - (top+1)
+            size = 2u << top;
+            const uint32_t m = depth - (D - (top + 1u));
             depth -= m;
-            c0 >>= m;
-            c1 >>= m;
-            c2 >>= m;
+            l0 = n0 & ~(size - 1u);
+            l1 = n1 & ~(size - 1u);
+            l2 = n2 & ~(size - 1u);
             // m == 1: the ancestor is the node we are iterating (still in `node`)
             if (m > 1 || (S.opt & kOptNoParentReuse)) node = depth ? stk[(depth - 1) * kBlockThreads] : S.root;
             t = texit;
