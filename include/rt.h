@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 typedef struct rt_renderer rt_renderer;
 
@@ -77,6 +77,8 @@ enum {
     RT_FLAG_NO_JITTER = 1u << 1,   /* force jitter off */
     RT_FLAG_RADIANCE = 1u << 2,    /* also keep the float4 mean radiance buffer */
     RT_FLAG_NO_SHADOWS = 1u << 3,  /* skip shadow rays (Lambert without visibility) */
+    RT_FLAG_HOST_BUILD = 1u << 4,  /* build the octree on the host (default: on the GPU);
+                                      both builders produce the identical tree */
     /* bits 16..19: scene-kernel variant for A/B runs (0 = default = 1, one ray
      * per lane; 2 = 64-ray wave packets); images are identical */
     RT_FLAG_VARIANT_SHIFT = 16,
@@ -127,9 +129,14 @@ typedef struct rt_scene_info {
     uint32_t prim_bytes;     /* bytes read per sphere test                              */
     float root_min[3];       /* effective root box: the configured box grown to          */
     float root_max[3];       /*   enclose every sphere (equal to it when none protrudes)  */
-    double build_ms;         /* host build time                                         */
-    double upload_ms;        /* host->device upload time                                */
+    double build_ms;         /* time to a device-resident octree (GPU build, or host
+                                build + upload with RT_FLAG_HOST_BUILD)                 */
+    double upload_ms;        /* time to place the sphere list in device memory          */
+    uint32_t builder;        /* RT_BUILDER_* that built the current tree                */
+    uint32_t reserved;
 } rt_scene_info;
+
+enum { RT_BUILDER_DEVICE = 0, RT_BUILDER_HOST = 1 };
 
 /* ---- version / discovery -------------------------------------------------- */
 int rt_abi_version(void);
@@ -163,13 +170,36 @@ void rt_resize_intrinsic(uint32_t width, uint32_t height, float K_out[9]);
  * parameters.  Builds the octree on the host and uploads it. */
 int rt_set_scene(rt_renderer* r, const float* spheres, const uint32_t* albedo, uint32_t n,
                  const rt_octree_params* oct);
+/* Same, from a sphere list already in device memory (e.g. produced by a
+ * simulation on the GPU): dev_spheres = 4*n floats, dev_albedo = n RGBA8 words
+ * or NULL.  `stream` (or NULL) is the stream that produced them; the call waits
+ * for it.  The octree is built on the GPU unless RT_FLAG_HOST_BUILD is set.
+ * Invalid spheres (r <= 0, non-finite values) are found on the device and the
+ * call fails with RT_E_INVALID, keeping the previous scene.  SURVEY.md 8f F1;
+ * the reference's intended entry is setOctree (include/renderer.cuh:35). */
+int rt_set_scene_device(rt_renderer* r, const void* dev_spheres, const void* dev_albedo,
+                        uint32_t n, const rt_octree_params* oct, void* stream);
 /* Mirror of the reference's setOctree(min, max, resolution): rebuilds the
  * octree of the current spheres with a new root box / resolution. */
 int rt_set_octree(rt_renderer* r, const float min[3], const float max[3], float resolution);
 int rt_get_scene_info(const rt_renderer* r, rt_scene_info* info);
+/* Copy the current octree to host memory (sizes from rt_get_scene_info):
+ * nodes_out 2*n_nodes words (uint2 records), prim_sp_out
+ * 4*n_prim_refs floats, prim_idx_out n_prim_refs words; any may be NULL. */
+int rt_export_octree(rt_renderer* r, uint32_t* nodes_out, float* prim_sp_out,
+                     uint32_t* prim_idx_out);
 /* Synthetic scene generator: splitmix64 -> PCG32 from `seed`;
  * centres U[0,1.28)^3, radius 0.02*(1000/n)^(1/3)*U[0.5,1), albedo U[0.2,1). */
 int rt_generate_spheres(uint32_t n, uint32_t seed, float* spheres_out, uint32_t* albedo_out);
+
+/* ---- scene files (binary sphere list) --------------------- */
+/* Write n spheres (4 floats each) and, if albedo != NULL, their RGBA8 words. */
+int rt_save_spheres(const char* path, const float* spheres, const uint32_t* albedo, uint32_t n);
+/* Read a sphere file.  *n_out = its sphere count; with spheres_out == NULL only
+ * the count is returned.  Otherwise capacity must be >= the count; albedo_out
+ * (may be NULL) gets the file's colours or 0.8 grey when it has none. */
+int rt_load_spheres(const char* path, float* spheres_out, uint32_t* albedo_out,
+                    uint32_t capacity, uint32_t* n_out);
 
 /* ---- render --------------------------------------------------------------- */
 /* Render one frame.  dev_rgba8: W*H*4 device bytes (e.g. the pointer a GL PBO

@@ -44,6 +44,7 @@ def load() -> ctypes.CDLL:
         "orc_scene_info": (None, [_P, _P]),
         "orc_depth_for_resolution": (_u32, [_P, _P, _f]),
         "orc_scene_root": (None, [_P, _P, _P]),
+        "orc_scene_export_bfs": (None, [_P, _P, _P]),
         "orc_trace": (ctypes.c_int, [_P, _P, _P, _f, _f, ctypes.c_int, _P, _P, _P]),
         "orc_trace_brute": (ctypes.c_int, [_P, _P, _P, _f, _f, ctypes.c_int, _P, _P]),
         "orc_render_scene": (None, [_P, _u32, _u32, _P, _P, _u32, _u32, _u32, _P, _f, _u32, _u32,
@@ -121,6 +122,14 @@ class Scene:
         b = np.zeros(3, np.float32)
         load().orc_scene_root(self._h, _p(a), _p(b))
         return a, b
+
+    def export_bfs(self):
+        """(nodes (n,2) uint32, prim_idx (m,) uint32) in the product's record layout."""
+        inf = self.info()
+        nodes = np.zeros((max(inf["n_nodes"], 1), 2), np.uint32)
+        idx = np.zeros(max(inf["n_prim_refs"], 1), np.uint32)
+        load().orc_scene_export_bfs(self._h, _p(nodes), _p(idx))
+        return nodes[:inf["n_nodes"]], idx[:inf["n_prim_refs"]]
 
     def trace(self, o, d, tmin=0.0, tmax=float("inf"), any_hit=False, brute=False):
         lib = load()

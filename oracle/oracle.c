@@ -360,6 +360,37 @@ void orc_scene_info(const orc_scene* s, uint32_t info[4]) {
     info[3] = s->depth_reached;
 }
 
+/* Breadth-first renumbering of the recursive tree: a node's children get
+ * consecutive slots in child order, leaf lists are laid out in slot order;
+ * internal record {first child slot, valid | leaf mask << 8}, leaf record
+ * {list offset, count}. */
+void orc_scene_export_bfs(const orc_scene* s, uint32_t* nodes_out, uint32_t* prim_idx_out) {
+    uint32_t* queue = (uint32_t*)malloc(sizeof(uint32_t) * (s->n_nodes ? s->n_nodes : 1));
+    uint32_t head = 0, tail = 0, prim = 0;
+    queue[tail++] = 0;
+    while (head < tail) {
+        const uint32_t slot = head;
+        const onode* nd = &s->nodes[queue[head++]];
+        if (nd->leaf) {
+            nodes_out[2 * slot] = prim;
+            nodes_out[2 * slot + 1] = nd->cnt;
+            for (uint32_t i = 0; i < nd->cnt; ++i) prim_idx_out[prim++] = s->prims[nd->off + i];
+            continue;
+        }
+        uint32_t valid = 0, leafm = 0;
+        const uint32_t first = tail;
+        for (int ch = 0; ch < 8; ++ch) {
+            if (nd->child[ch] < 0) continue;
+            valid |= 1u << ch;
+            if (s->nodes[nd->child[ch]].leaf) leafm |= 1u << ch;
+            queue[tail++] = (uint32_t)nd->child[ch];
+        }
+        nodes_out[2 * slot] = first;
+        nodes_out[2 * slot + 1] = valid | (leafm << 8);
+    }
+    free(queue);
+}
+
 void orc_scene_root(const orc_scene* s, float rmin[3], float rmax[3]) {
     for (int i = 0; i < 3; ++i) {
         rmin[i] = s->rmin[i];

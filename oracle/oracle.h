@@ -43,6 +43,10 @@ void orc_scene_free(orc_scene* s);
 void orc_scene_info(const orc_scene* s, uint32_t info[4]);
 /* effective root box (configured box grown to enclose every sphere) */
 void orc_scene_root(const orc_scene* s, float rmin[3], float rmax[3]);
+/* The tree in the product's breadth-first record layout:
+ * nodes_out 2*info[0] words, prim_idx_out info[2] words.  Lets tests compare
+ * a built octree with this one record for record. */
+void orc_scene_export_bfs(const orc_scene* s, uint32_t* nodes_out, uint32_t* prim_idx_out);
 uint32_t orc_depth_for_resolution(const float root_min[3], const float root_max[3], float res);
 
 /* counters[0]=primary rays, [1]=shadow rays, [2]=nodes visited, [3]=prims tested */

@@ -29,6 +29,9 @@ RT_FLAG_JITTER = 1 << 0
 RT_FLAG_NO_JITTER = 1 << 1
 RT_FLAG_RADIANCE = 1 << 2
 RT_FLAG_NO_SHADOWS = 1 << 3
+RT_FLAG_HOST_BUILD = 1 << 4
+RT_BUILDER_DEVICE = 0
+RT_BUILDER_HOST = 1
 RT_FLAG_VARIANT_SHIFT = 16
 RT_FLAG_OPT_SHIFT = 20
 VARIANT_LANE = 1    # one ray per lane
@@ -89,10 +92,13 @@ class RtSceneInfo(ctypes.Structure):
         ("root_max", _f3),
         ("build_ms", ctypes.c_double),
         ("upload_ms", ctypes.c_double),
+        ("builder", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
     ]
 
     def as_dict(self) -> dict:
-        d = {f: getattr(self, f) for f, _ in self._fields_}
+        d = {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+        d["builder"] = "host" if self.builder == RT_BUILDER_HOST else "device"
         d["root_min"] = list(self.root_min)
         d["root_max"] = list(self.root_max)
         return d
@@ -116,8 +122,12 @@ SIGNATURES = {
     "rt_resize": (_int, [_P, _u32, _u32]),
     "rt_resize_intrinsic": (None, [_u32, _u32, _fp]),
     "rt_set_scene": (_int, [_P, _P, _P, _u32, ctypes.POINTER(RtOctreeParams)]),
+    "rt_set_scene_device": (_int, [_P, _P, _P, _u32, ctypes.POINTER(RtOctreeParams), _P]),
     "rt_set_octree": (_int, [_P, _fp, _fp, ctypes.c_float]),
     "rt_get_scene_info": (_int, [_P, ctypes.POINTER(RtSceneInfo)]),
+    "rt_export_octree": (_int, [_P, _P, _P, _P]),
+    "rt_save_spheres": (_int, [ctypes.c_char_p, _P, _P, _u32]),
+    "rt_load_spheres": (_int, [ctypes.c_char_p, _P, _P, _u32, ctypes.POINTER(_u32)]),
     "rt_generate_spheres": (_int, [_u32, _u32, _P, _P]),
     "rt_render": (_int, [_P, _P, _P, ctypes.POINTER(RtStats)]),
     "rt_render_tiles": (_int, [_P, _P, _u32, _u32, _P, _P, ctypes.POINTER(RtStats)]),

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/rt.h"
+#include "octree_gpu.h"
 #include "rt_params.h"
 #include "scene_build.h"
 
@@ -58,11 +59,14 @@ struct rt_renderer {
     std::vector<uint32_t> tiles_host;  // its host copy (source of the async upload)
     DevBuf<uint32_t> utiles;         // tile list for rt_unpack_tiles
     std::vector<uint32_t> utiles_host;
-    // scene (host copies + device arrays)
+    // scene: the sphere list lives in d_spheres/d_albedo; `spheres` is a host
+    // copy when the scene came from host memory (host builder input)
+    uint32_t n_spheres = 0;
     std::vector<float> spheres;
-    std::vector<uint32_t> albedo;
+    bool host_copy = false;
     rt_octree_params oct;
     bool has_scene = false;
+    GpuOctreeBuilder gpu_build;
     DevBuf<uint2> d_nodes;
     DevBuf<float4> d_prim_sp;
     DevBuf<uint32_t> d_prim_idx;
@@ -144,67 +148,109 @@ void fill_frame_args(rt_renderer* r, FrameArgs& a) {
     a.variant = v ? v : (a.spp >= 8u ? kVariantLaneUnified2NoStats : kVariantLaneUnified);
 }
 
-int upload_scene(rt_renderer* r) {
-    const uint32_t n = static_cast<uint32_t>(r->albedo.size());
+// Build the octree of the device sphere list (d_spheres) and point the
+// kernel's scene arguments at it.  The device builder is the default; the
+// host builder (RT_FLAG_HOST_BUILD) yields the identical tree.
+int build_scene(rt_renderer* r) {
+    const uint32_t n = r->n_spheres;
     rt_octree_params& p = r->oct;
     uint32_t depth = p.max_depth ? p.max_depth : depth_for_resolution(p.min, p.max, p.resolution);
     if (depth > kMaxDepth) depth = kMaxDepth;
-    auto t0 = std::chrono::steady_clock::now();
-    BuiltOctree tree;
-    build_octree(r->spheres.data(), n, p.min, p.max, depth, p.leaf_capacity ? p.leaf_capacity : 8,
-                 tree);
-    auto t1 = std::chrono::steady_clock::now();
+    const uint32_t cap = p.leaf_capacity ? p.leaf_capacity : 8;
     int st;
     if ((st = set_device(r))) return st;
-    const size_t nn = tree.nodes.size(), np = tree.prim_idx.size();
-    if ((st = ensure(r, r->d_nodes, nn))) return st;
-    if ((st = ensure(r, r->d_prim_sp, np))) return st;
-    if ((st = ensure(r, r->d_prim_idx, np))) return st;
-    if ((st = ensure(r, r->d_spheres, n))) return st;
-    if ((st = ensure(r, r->d_albedo, n))) return st;
-    RT_HIP(r, hipMemcpy(r->d_nodes.p, tree.nodes.data(), nn * sizeof(uint2), hipMemcpyHostToDevice));
-    if (np) {
-        RT_HIP(r, hipMemcpy(r->d_prim_sp.p, tree.prim_sp.data(), np * sizeof(float4),
-                            hipMemcpyHostToDevice));
-        RT_HIP(r, hipMemcpy(r->d_prim_idx.p, tree.prim_idx.data(), np * sizeof(uint32_t),
-                            hipMemcpyHostToDevice));
-    }
-    if (n) {
-        RT_HIP(r, hipMemcpy(r->d_spheres.p, r->spheres.data(), n * sizeof(float4),
-                            hipMemcpyHostToDevice));
-        RT_HIP(r, hipMemcpy(r->d_albedo.p, r->albedo.data(), n * sizeof(uint32_t),
-                            hipMemcpyHostToDevice));
-    }
-    auto t2 = std::chrono::steady_clock::now();
-
+    // buffers of the previous tree may still be read by frames in flight on
+    // any stream: the rebuild waits for the device
+    RT_HIP(r, hipDeviceSynchronize());
+    r->has_scene = false;
+    rt_scene_info& in = r->info;
+    const double upload_ms = in.upload_ms;
+    in = rt_scene_info();
+    in.upload_ms = upload_ms;
     SceneArgs& sc = r->sc;
-    sc.nodes = r->d_nodes.p;
-    sc.prim_sp = r->d_prim_sp.p;
-    sc.prim_idx = r->d_prim_idx.p;
+    float rmin[3], rmax[3];
+    auto t0 = std::chrono::steady_clock::now();
+    if (r->cfg.flags & RT_FLAG_HOST_BUILD) {
+        if (!r->host_copy) {
+            r->spheres.resize(4u * n);
+            if (n)
+                RT_HIP(r, hipMemcpy(r->spheres.data(), r->d_spheres.p, n * sizeof(float4),
+                                    hipMemcpyDeviceToHost));
+            r->host_copy = true;
+        }
+        BuiltOctree tree;
+        build_octree(r->spheres.data(), n, p.min, p.max, depth, cap, tree);
+        const size_t nn = tree.nodes.size(), np = tree.prim_idx.size();
+        if ((st = ensure(r, r->d_nodes, nn))) return st;
+        if ((st = ensure(r, r->d_prim_sp, np))) return st;
+        if ((st = ensure(r, r->d_prim_idx, np))) return st;
+        RT_HIP(r, hipMemcpy(r->d_nodes.p, tree.nodes.data(), nn * sizeof(uint2),
+                            hipMemcpyHostToDevice));
+        if (np) {
+            RT_HIP(r, hipMemcpy(r->d_prim_sp.p, tree.prim_sp.data(), np * sizeof(float4),
+                                hipMemcpyHostToDevice));
+            RT_HIP(r, hipMemcpy(r->d_prim_idx.p, tree.prim_idx.data(), np * sizeof(uint32_t),
+                                hipMemcpyHostToDevice));
+        }
+        sc.nodes = r->d_nodes.p;
+        sc.prim_sp = r->d_prim_sp.p;
+        sc.prim_idx = r->d_prim_idx.p;
+        sc.root = make_uint2(tree.nodes[0].x, tree.nodes[0].y);
+        sc.root_is_leaf = tree.root_is_leaf ? 1u : 0u;
+        in.n_nodes = static_cast<uint32_t>(nn);
+        in.n_leaves = tree.n_leaves;
+        in.n_prim_refs = static_cast<uint32_t>(np);
+        in.depth_reached = tree.depth_reached;
+        in.builder = RT_BUILDER_HOST;
+        memcpy(rmin, tree.rmin, sizeof(rmin));
+        memcpy(rmax, tree.rmax, sizeof(rmax));
+    } else {
+        GpuBuildResult res;
+        hipError_t e = r->gpu_build.build(r->d_spheres.p, n, p.min, p.max, depth, cap, r->stream, &res);
+        if (e != hipSuccess) return hip_fail(r, e, "device octree build");
+        if (res.n_invalid)
+            return fail(r, RT_E_INVALID, "scene has spheres with radius <= 0 or non-finite values");
+        sc.nodes = r->gpu_build.nodes();
+        sc.prim_sp = r->gpu_build.prim_sp();
+        sc.prim_idx = r->gpu_build.prim_idx();
+        sc.root = res.root;
+        sc.root_is_leaf = res.root_is_leaf ? 1u : 0u;
+        in.n_nodes = res.n_nodes;
+        in.n_leaves = res.n_leaves;
+        in.n_prim_refs = res.n_prims;
+        in.depth_reached = res.depth_reached;
+        in.builder = RT_BUILDER_DEVICE;
+        memcpy(rmin, res.rmin, sizeof(rmin));
+        memcpy(rmax, res.rmax, sizeof(rmax));
+    }
+    auto t1 = std::chrono::steady_clock::now();
     sc.spheres = r->d_spheres.p;
     sc.albedo = r->d_albedo.p;
-    sc.root = make_uint2(tree.nodes[0].x, tree.nodes[0].y);
-    sc.root_is_leaf = tree.root_is_leaf ? 1u : 0u;
     sc.max_depth = depth;
     sc.G = static_cast<float>(1u << depth);
     for (int i = 0; i < 3; ++i) {
-        sc.rmin[i] = tree.rmin[i];
-        sc.scale[i] = sc.G / (tree.rmax[i] - tree.rmin[i]);
-        r->info.root_min[i] = tree.rmin[i];
-        r->info.root_max[i] = tree.rmax[i];
+        sc.rmin[i] = rmin[i];
+        sc.scale[i] = sc.G / (rmax[i] - rmin[i]);
+        in.root_min[i] = rmin[i];
+        in.root_max[i] = rmax[i];
     }
-    rt_scene_info& in = r->info;
     in.n_spheres = n;
-    in.n_nodes = static_cast<uint32_t>(nn);
-    in.n_leaves = tree.n_leaves;
-    in.n_prim_refs = static_cast<uint32_t>(np);
     in.max_depth = depth;
-    in.depth_reached = tree.depth_reached;
     in.node_bytes = sizeof(uint2);
     in.prim_bytes = sizeof(float4) + sizeof(uint32_t);
     in.build_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-    in.upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
     r->has_scene = true;
+    return RT_OK;
+}
+
+int check_octree_params(rt_renderer* r, const rt_octree_params* oct, const char* who) {
+    if (!oct) return RT_OK;
+    for (int i = 0; i < 3; ++i)
+        if (!(oct->max[i] > oct->min[i]))
+            return fail(r, RT_E_INVALID, std::string(who) + ": empty octree root box");
+    if (oct->max_depth > kMaxDepth) return fail(r, RT_E_INVALID, std::string(who) + ": max_depth > 16");
+    if (oct->max_depth == 0 && !(oct->resolution > 0.0f))
+        return fail(r, RT_E_INVALID, std::string(who) + ": need max_depth or resolution > 0");
     return RT_OK;
 }
 
@@ -371,6 +417,7 @@ int rt_destroy(rt_renderer* r) {
     r->d_prim_idx.release();
     r->d_spheres.release();
     r->d_albedo.release();
+    r->gpu_build.release();
     if (r->ev0) (void)hipEventDestroy(r->ev0);
     if (r->ev1) (void)hipEventDestroy(r->ev1);
     if (r->stream) (void)hipStreamDestroy(r->stream);
@@ -417,24 +464,74 @@ int rt_set_scene(rt_renderer* r, const float* spheres, const uint32_t* albedo, u
                  const rt_octree_params* oct) {
     if (!r) return fail(r, RT_E_INVALID, "rt_set_scene: null handle");
     if (n && !spheres) return fail(r, RT_E_INVALID, "rt_set_scene: null spheres");
-    if (oct) {
-        for (int i = 0; i < 3; ++i)
-            if (!(oct->max[i] > oct->min[i]))
-                return fail(r, RT_E_INVALID, "rt_set_scene: empty octree root box");
-        if (oct->max_depth > kMaxDepth)
-            return fail(r, RT_E_INVALID, "rt_set_scene: max_depth > 16");
-        if (oct->max_depth == 0 && !(oct->resolution > 0.0f))
-            return fail(r, RT_E_INVALID, "rt_set_scene: need max_depth or resolution > 0");
-        r->oct = *oct;
+    int st;
+    if ((st = check_octree_params(r, oct, "rt_set_scene"))) return st;
+    for (uint32_t i = 0; i < n; ++i) {
+        const float* s = spheres + 4u * i;
+        if (!(s[3] > 0.0f) || !isfinite(s[0]) || !isfinite(s[1]) || !isfinite(s[2]) ||
+            !isfinite(s[3]))
+            return fail(r, RT_E_INVALID,
+                        "rt_set_scene: sphere with radius <= 0 or non-finite values");
     }
-    for (uint32_t i = 0; i < n; ++i)
-        if (!(spheres[4 * i + 3] > 0.0f) || !isfinite(spheres[4 * i]) ||
-            !isfinite(spheres[4 * i + 1]) || !isfinite(spheres[4 * i + 2]))
-            return fail(r, RT_E_INVALID, "rt_set_scene: sphere with radius <= 0 or non-finite centre");
+    if (oct) r->oct = *oct;
+    if ((st = set_device(r))) return st;
+    RT_HIP(r, hipDeviceSynchronize());
+    auto t0 = std::chrono::steady_clock::now();
     r->spheres.assign(spheres, spheres + 4u * n);
-    r->albedo.resize(n);
-    for (uint32_t i = 0; i < n; ++i) r->albedo[i] = albedo ? albedo[i] : 0xFFCCCCCCu;
-    return upload_scene(r);
+    r->host_copy = true;
+    r->n_spheres = n;
+    std::vector<uint32_t> alb(n);
+    for (uint32_t i = 0; i < n; ++i) alb[i] = albedo ? albedo[i] : 0xFFCCCCCCu;
+    if ((st = ensure(r, r->d_spheres, n))) return st;
+    if ((st = ensure(r, r->d_albedo, n))) return st;
+    if (n) {
+        RT_HIP(r, hipMemcpy(r->d_spheres.p, spheres, n * sizeof(float4), hipMemcpyHostToDevice));
+        RT_HIP(r, hipMemcpy(r->d_albedo.p, alb.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
+    r->info.upload_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return build_scene(r);
+}
+
+int rt_set_scene_device(rt_renderer* r, const void* dev_spheres, const void* dev_albedo,
+                        uint32_t n, const rt_octree_params* oct, void* stream) {
+    if (!r) return fail(r, RT_E_INVALID, "rt_set_scene_device: null handle");
+    if (n && !dev_spheres) return fail(r, RT_E_INVALID, "rt_set_scene_device: null spheres");
+    int st;
+    if ((st = check_octree_params(r, oct, "rt_set_scene_device"))) return st;
+    if ((st = set_device(r))) return st;
+    if (stream) RT_HIP(r, hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    const float4* src = static_cast<const float4*>(dev_spheres);
+    if (n) {
+        SphereBounds sb;
+        hipError_t e = r->gpu_build.bounds(src, n, r->stream, &sb);
+        if (e != hipSuccess) return hip_fail(r, e, "rt_set_scene_device: validation");
+        if (sb.n_invalid)
+            return fail(r, RT_E_INVALID,
+                        "rt_set_scene_device: sphere with radius <= 0 or non-finite values");
+    }
+    if (oct) r->oct = *oct;
+    RT_HIP(r, hipDeviceSynchronize());
+    auto t0 = std::chrono::steady_clock::now();
+    if ((st = ensure(r, r->d_spheres, n))) return st;
+    if ((st = ensure(r, r->d_albedo, n))) return st;
+    if (n) {
+        RT_HIP(r, hipMemcpyAsync(r->d_spheres.p, src, n * sizeof(float4), hipMemcpyDeviceToDevice,
+                                 r->stream));
+        if (dev_albedo)
+            RT_HIP(r, hipMemcpyAsync(r->d_albedo.p, dev_albedo, n * sizeof(uint32_t),
+                                     hipMemcpyDeviceToDevice, r->stream));
+        else
+            RT_HIP(r, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(r->d_albedo.p),
+                                        0xFFCCCCCCu, n, r->stream));
+        RT_HIP(r, hipStreamSynchronize(r->stream));
+    }
+    r->n_spheres = n;
+    r->spheres.clear();
+    r->host_copy = false;
+    r->info.upload_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return build_scene(r);
 }
 
 int rt_set_octree(rt_renderer* r, const float mn[3], const float mx[3], float resolution) {
@@ -449,14 +546,48 @@ int rt_set_octree(rt_renderer* r, const float mn[3], const float mx[3], float re
     p.resolution = resolution;
     p.max_depth = 0;
     r->oct = p;
-    if (!r->has_scene && r->spheres.empty()) return RT_OK;
-    return upload_scene(r);
+    if (!r->has_scene) return RT_OK;
+    return build_scene(r);
 }
 
 int rt_get_scene_info(const rt_renderer* r, rt_scene_info* info) {
     if (!r || !info) return RT_E_INVALID;
     if (!r->has_scene) return RT_E_NOSCENE;
     *info = r->info;
+    return RT_OK;
+}
+
+int rt_export_octree(rt_renderer* r, uint32_t* nodes_out, float* prim_sp_out,
+                     uint32_t* prim_idx_out) {
+    if (!r) return fail(r, RT_E_INVALID, "rt_export_octree: null handle");
+    if (!r->has_scene) return fail(r, RT_E_NOSCENE, "rt_export_octree: no scene");
+    int st;
+    if ((st = set_device(r))) return st;
+    RT_HIP(r, hipDeviceSynchronize());
+    const size_t nn = r->info.n_nodes, np = r->info.n_prim_refs;
+    if (nodes_out)
+        RT_HIP(r, hipMemcpy(nodes_out, r->sc.nodes, nn * sizeof(uint2), hipMemcpyDeviceToHost));
+    if (prim_sp_out && np)
+        RT_HIP(r, hipMemcpy(prim_sp_out, r->sc.prim_sp, np * sizeof(float4), hipMemcpyDeviceToHost));
+    if (prim_idx_out && np)
+        RT_HIP(r, hipMemcpy(prim_idx_out, r->sc.prim_idx, np * sizeof(uint32_t),
+                            hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_save_spheres(const char* path, const float* spheres, const uint32_t* albedo, uint32_t n) {
+    if (!path || (n && !spheres)) return fail(nullptr, RT_E_INVALID, "rt_save_spheres: null argument");
+    std::string err;
+    if (!save_sphere_file(path, spheres, albedo, n, &err)) return fail(nullptr, RT_E_INVALID, err);
+    return RT_OK;
+}
+
+int rt_load_spheres(const char* path, float* spheres_out, uint32_t* albedo_out, uint32_t capacity,
+                    uint32_t* n_out) {
+    if (!path || !n_out) return fail(nullptr, RT_E_INVALID, "rt_load_spheres: null argument");
+    std::string err;
+    if (!load_sphere_file(path, spheres_out, albedo_out, capacity, n_out, &err))
+        return fail(nullptr, RT_E_INVALID, err);
     return RT_OK;
 }
 

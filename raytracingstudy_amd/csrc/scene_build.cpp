@@ -8,6 +8,7 @@
 #include "scene_build.h"
 
 #include <math.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
@@ -205,6 +206,103 @@ void build_octree(const float* spheres, uint32_t n, const float rmin[3], const f
         }
         level.swap(next);
     }
+}
+
+namespace {
+
+constexpr char kSphereMagic[8] = {'R', 'T', 'S', 'P', 'H', 'E', 'R', 'E'};
+constexpr uint32_t kSphereVersion = 1, kSphereHeader = 32;
+
+void put32(unsigned char* p, uint32_t v) {
+    for (int i = 0; i < 4; ++i) p[i] = static_cast<unsigned char>(v >> (8 * i));
+}
+uint32_t get32(const unsigned char* p) {
+    return uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
+}
+
+struct File {
+    FILE* f;
+    explicit File(FILE* x) : f(x) {}
+    ~File() {
+        if (f) fclose(f);
+    }
+};
+
+}  // namespace
+
+bool save_sphere_file(const char* path, const float* spheres, const uint32_t* albedo, uint32_t n,
+                      std::string* err) {
+    File f(fopen(path, "wb"));
+    if (!f.f) {
+        *err = std::string("cannot open ") + path + " for writing";
+        return false;
+    }
+    unsigned char h[kSphereHeader] = {0};
+    memcpy(h, kSphereMagic, 8);
+    put32(h + 8, kSphereVersion);
+    put32(h + 12, n);
+    put32(h + 16, albedo ? 1u : 0u);
+    put32(h + 20, kSphereHeader);
+    bool ok = fwrite(h, 1, sizeof(h), f.f) == sizeof(h);
+    // payload little-endian: the host (x86-64) order, written as is
+    if (ok && n) ok = fwrite(spheres, sizeof(float) * 4, n, f.f) == n;
+    if (ok && n && albedo) ok = fwrite(albedo, sizeof(uint32_t), n, f.f) == n;
+    if (ok) ok = fflush(f.f) == 0;
+    if (!ok) *err = std::string("write error on ") + path;
+    return ok;
+}
+
+bool load_sphere_file(const char* path, float* spheres, uint32_t* albedo, uint32_t capacity,
+                      uint32_t* n_out, std::string* err) {
+    File f(fopen(path, "rb"));
+    if (!f.f) {
+        *err = std::string("cannot open ") + path;
+        return false;
+    }
+    unsigned char h[kSphereHeader];
+    if (fread(h, 1, sizeof(h), f.f) != sizeof(h) || memcmp(h, kSphereMagic, 8) != 0) {
+        *err = std::string(path) + ": not a sphere file (bad magic)";
+        return false;
+    }
+    const uint32_t ver = get32(h + 8), n = get32(h + 12), flags = get32(h + 16),
+                   hb = get32(h + 20);
+    if (ver != kSphereVersion || hb != kSphereHeader || (flags & ~1u)) {
+        *err = std::string(path) + ": unsupported sphere file version/header";
+        return false;
+    }
+    const bool has_albedo = flags & 1u;
+    if (fseek(f.f, 0, SEEK_END) != 0) {
+        *err = std::string(path) + ": cannot seek";
+        return false;
+    }
+    const long size = ftell(f.f);
+    const uint64_t want = kSphereHeader + uint64_t(n) * 16u + (has_albedo ? uint64_t(n) * 4u : 0u);
+    if (size < 0 || uint64_t(size) != want) {
+        *err = std::string(path) + ": file size does not match its sphere count";
+        return false;
+    }
+    *n_out = n;
+    if (!spheres) return true;
+    if (capacity < n) {
+        *err = std::string(path) + ": capacity smaller than the sphere count";
+        return false;
+    }
+    fseek(f.f, kSphereHeader, SEEK_SET);
+    if (n && fread(spheres, sizeof(float) * 4, n, f.f) != n) {
+        *err = std::string(path) + ": short read";
+        return false;
+    }
+    if (albedo) {
+        if (has_albedo) {
+            if (n && fread(albedo, sizeof(uint32_t), n, f.f) != n) {
+                *err = std::string(path) + ": short read";
+                return false;
+            }
+        } else {
+            for (uint32_t i = 0; i < n; ++i) albedo[i] = 0xFFCCCCCCu;
+        }
+    }
+    return true;
 }
 
 }  // namespace rtamd

@@ -2,6 +2,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <string>
 #include <vector>
 
 namespace rtamd {
@@ -33,5 +34,16 @@ void build_octree(const float* spheres, uint32_t n, const float rmin[3], const f
 uint32_t depth_for_resolution(const float rmin[3], const float rmax[3], float res);
 
 uint32_t mix32(uint32_t x);
+
+// Binary sphere list: a 32-byte little-endian header
+// {"RTSPHERE", u32 version = 1, u32 n, u32 flags (bit 0: albedo present),
+// u32 header bytes = 32, u64 0}, then n x {f32 cx, cy, cz, r}, then n x u32
+// RGBA8 when flag bit 0 is set.
+bool save_sphere_file(const char* path, const float* spheres, const uint32_t* albedo, uint32_t n,
+                      std::string* err);
+// spheres == nullptr: only *n_out.  Otherwise capacity >= n; albedo may be
+// nullptr; missing colours read as 0.8 grey.
+bool load_sphere_file(const char* path, float* spheres, uint32_t* albedo, uint32_t capacity,
+                      uint32_t* n_out, std::string* err);
 
 }  // namespace rtamd

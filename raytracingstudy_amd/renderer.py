@@ -28,11 +28,13 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import (RT_FLAG_JITTER, RT_FLAG_NO_JITTER, RT_FLAG_NO_SHADOWS, RT_FLAG_RADIANCE,
+from ._lib import (RT_FLAG_HOST_BUILD, RT_FLAG_JITTER, RT_FLAG_NO_JITTER, RT_FLAG_NO_SHADOWS,
+                   RT_FLAG_RADIANCE,
                    RT_MODE_COMPAT, RT_MODE_SCENE, RtConfig, RtOctreeParams, RtSceneInfo,
                    RtStats, check)
 
-__all__ = ["KernelRenderer", "resize_intrinsic", "generate_spheres", "device_count"]
+__all__ = ["KernelRenderer", "resize_intrinsic", "generate_spheres", "device_count",
+           "save_spheres", "load_spheres"]
 
 _MODES = {"compat": RT_MODE_COMPAT, "scene": RT_MODE_SCENE}
 
@@ -64,6 +66,38 @@ def generate_spheres(n: int, seed: int = 0x2545F491):
     return sp[:n], al[:n]
 
 
+def save_spheres(path: str, spheres: np.ndarray, albedo: Optional[np.ndarray] = None) -> None:
+    """Write a binary sphere file (rt_save_spheres; format in DESIGN.md §4.1)."""
+    sp = np.ascontiguousarray(spheres, np.float32).reshape(-1, 4)
+    al = None if albedo is None else np.ascontiguousarray(albedo, np.uint32).reshape(-1)
+    if al is not None and al.shape[0] != sp.shape[0]:
+        raise ValueError("albedo must have one entry per sphere")
+    check(_lib.load().rt_save_spheres(str(path).encode(), _vptr(sp), _vptr(al), sp.shape[0]))
+
+
+def load_spheres(path: str):
+    """Read a binary sphere file: ((n,4) float32 spheres, (n,) uint32 albedo)."""
+    lib = _lib.load()
+    n = ctypes.c_uint32(0)
+    check(lib.rt_load_spheres(str(path).encode(), None, None, 0, ctypes.byref(n)))
+    sp = np.zeros((max(n.value, 1), 4), np.float32)
+    al = np.zeros(max(n.value, 1), np.uint32)
+    check(lib.rt_load_spheres(str(path).encode(), _vptr(sp), _vptr(al), sp.shape[0],
+                              ctypes.byref(n)))
+    return sp[:n.value], al[:n.value]
+
+
+def _octree_params(root_min, root_max, resolution, max_depth, leaf_capacity) -> RtOctreeParams:
+    p = RtOctreeParams()
+    for i in range(3):
+        p.min[i] = float(root_min[i])
+        p.max[i] = float(root_max[i])
+    p.resolution = float(resolution)
+    p.max_depth = int(max_depth)
+    p.leaf_capacity = int(leaf_capacity)
+    return p
+
+
 class KernelRenderer:
     """MI355X renderer handle (one per thread / stream)."""
 
@@ -71,7 +105,7 @@ class KernelRenderer:
                  seed: int = 0x2545F491, device: int = -1, jitter: Optional[bool] = None,
                  shadows: bool = True, radiance: bool = False,
                  light_dir: Sequence[float] = (1.0, 1.0, -1.0), ambient: float = 0.1,
-                 variant: int = 0, opt_off: int = 0):
+                 variant: int = 0, opt_off: int = 0, host_build: bool = False):
         lib = _lib.load()
         cfg = RtConfig()
         lib.rt_config_default(ctypes.byref(cfg))
@@ -89,6 +123,8 @@ class KernelRenderer:
             flags |= RT_FLAG_NO_SHADOWS
         if radiance:
             flags |= RT_FLAG_RADIANCE
+        if host_build:
+            flags |= RT_FLAG_HOST_BUILD
         flags |= (int(variant) & 0xF) << _lib.RT_FLAG_VARIANT_SHIFT
         flags |= (int(opt_off) & 0xF) << _lib.RT_FLAG_OPT_SHIFT
         cfg.flags = flags
@@ -145,16 +181,39 @@ class KernelRenderer:
         al = None if albedo is None else np.ascontiguousarray(albedo, np.uint32).reshape(-1)
         if al is not None and al.shape[0] != sp.shape[0]:
             raise ValueError("albedo must have one entry per sphere")
-        p = RtOctreeParams()
-        for i in range(3):
-            p.min[i] = float(root_min[i])
-            p.max[i] = float(root_max[i])
-        p.resolution = float(resolution)
-        p.max_depth = int(max_depth)
-        p.leaf_capacity = int(leaf_capacity)
+        p = _octree_params(root_min, root_max, resolution, max_depth, leaf_capacity)
         check(self._lib.rt_set_scene(self._h, _vptr(sp), _vptr(al), sp.shape[0], ctypes.byref(p)),
               self._h)
         return self.scene_info()
+
+    def set_scene_device(self, spheres_ptr: int, n: int, albedo_ptr: Optional[int] = None, *,
+                         stream: Optional[int] = None, root_min=(0.0, 0.0, 0.0),
+                         root_max=(1.28, 1.28, 1.28), resolution: float = 0.01,
+                         max_depth: int = 0, leaf_capacity: int = 8) -> dict:
+        """Scene from a sphere list already in device memory (4*n float32 at
+        spheres_ptr, n RGBA8 words at albedo_ptr); the octree is built on the GPU."""
+        p = _octree_params(root_min, root_max, resolution, max_depth, leaf_capacity)
+        check(self._lib.rt_set_scene_device(
+            self._h, ctypes.c_void_p(spheres_ptr) if spheres_ptr else None,
+            ctypes.c_void_p(albedo_ptr) if albedo_ptr else None, int(n), ctypes.byref(p),
+            ctypes.c_void_p(stream) if stream else None), self._h)
+        return self.scene_info()
+
+    def set_scene_file(self, path: str, **octree) -> dict:
+        """Load a binary sphere file (load_spheres) and make it the scene."""
+        sp, al = load_spheres(path)
+        return self.set_scene(sp, al, **octree)
+
+    def export_octree(self):
+        """The device octree as host arrays: nodes (n,2) uint32 records, prim_sp
+        (m,4) float32, prim_idx (m,) uint32 (rt_export_octree)."""
+        info = self.scene_info()
+        nodes = np.zeros((max(info["n_nodes"], 1), 2), np.uint32)
+        m = info["n_prim_refs"]
+        sp = np.zeros((max(m, 1), 4), np.float32)
+        idx = np.zeros(max(m, 1), np.uint32)
+        check(self._lib.rt_export_octree(self._h, _vptr(nodes), _vptr(sp), _vptr(idx)), self._h)
+        return nodes[:info["n_nodes"]], sp[:m], idx[:m]
 
     def scene_info(self) -> dict:
         info = RtSceneInfo()
