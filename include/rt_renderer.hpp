@@ -76,6 +76,31 @@ public:
         check(rt_set_scene(r_, spheres.data(), albedo.empty() ? nullptr : albedo.data(), n, oct),
               r_);
     }
+    // new: sphere list already in device memory (built into an octree on the GPU)
+    void setSceneDevice(const void* dev_spheres, uint32_t n, const void* dev_albedo = nullptr,
+                        const rt_octree_params* oct = nullptr, void* stream = nullptr) {
+        check(rt_set_scene_device(r_, dev_spheres, dev_albedo, n, oct, stream), r_);
+    }
+    // new: binary sphere file (rt_save_spheres format)
+    void setSceneFile(const std::string& path, const rt_octree_params* oct = nullptr) {
+        std::vector<float> sp;
+        std::vector<uint32_t> al;
+        loadSpheres(path, sp, al);
+        setScene(sp, al, oct);
+    }
+    static void loadSpheres(const std::string& path, std::vector<float>& spheres,
+                            std::vector<uint32_t>& albedo) {
+        uint32_t n = 0;
+        check(rt_load_spheres(path.c_str(), nullptr, nullptr, 0, &n));
+        spheres.resize(4 * size_t(n));
+        albedo.resize(n);
+        check(rt_load_spheres(path.c_str(), spheres.data(), albedo.data(), n, &n));
+    }
+    static void saveSpheres(const std::string& path, const std::vector<float>& spheres,
+                            const std::vector<uint32_t>& albedo = {}) {
+        check(rt_save_spheres(path.c_str(), spheres.data(), albedo.empty() ? nullptr : albedo.data(),
+                              static_cast<uint32_t>(spheres.size() / 4)));
+    }
     rt_scene_info sceneInfo() const {
         rt_scene_info i;
         check(rt_get_scene_info(r_, &i), r_);

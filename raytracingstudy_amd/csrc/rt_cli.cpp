@@ -6,7 +6,8 @@
 // tests/test_native_cli.py and for rocprof runs without Python.
 //
 //   rt_cli [--config c1|c2|c3|c5] [--width W --height H --spp S --spheres N
-//           --depth D] [--frames F] [--out image.ppm]
+//           --depth D] [--frames F] [--out image.ppm] [--scene in.rtsph]
+//          [--save-scene out.rtsph] [--host-build]
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -18,7 +19,8 @@
 #include "../../include/rt_renderer.hpp"
 
 int main(int argc, char** argv) {
-    std::string cfg = "c2", out;
+    std::string cfg = "c2", out, scene_in, scene_out;
+    bool host_build = false;
     int W = 0, H = 0, spp = 0, frames = 3;
     long n = -1;
     int depth = 0;
@@ -38,6 +40,9 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--depth")) depth = atoi(next("--depth"));
         else if (!strcmp(argv[i], "--frames")) frames = atoi(next("--frames"));
         else if (!strcmp(argv[i], "--out")) out = next("--out");
+        else if (!strcmp(argv[i], "--scene")) scene_in = next("--scene");
+        else if (!strcmp(argv[i], "--save-scene")) scene_out = next("--save-scene");
+        else if (!strcmp(argv[i], "--host-build")) host_build = true;
         else {
             fprintf(stderr, "unknown argument %s\n", argv[i]);
             return 2;
@@ -68,6 +73,7 @@ int main(int argc, char** argv) {
         rc.height = H;
         rc.spp = spp;
         rc.mode = c->mode;
+        if (host_build) rc.flags |= RT_FLAG_HOST_BUILD;
         rtamd::KernelRenderer r(rc);
         r.resize(W, H);
         // Displayer default orientation (include/window/displayer.h:47-52):
@@ -76,17 +82,24 @@ int main(int argc, char** argv) {
         const float pose[16] = {1, 0, 0, 0, 0, -1, 0, 0, 0, 0, -1, 0,
                                 scene ? 0.64f : 0.f, scene ? 0.64f : 0.f, scene ? 2.2f : 3.f, 1};
         if (scene) {
-            std::vector<float> sp(4 * (size_t)n);
-            std::vector<uint32_t> al((size_t)n);
-            rtamd::check(rt_generate_spheres((uint32_t)n, 0x2545F491u, sp.data(), al.data()));
+            std::vector<float> sp;
+            std::vector<uint32_t> al;
+            if (!scene_in.empty()) {
+                rtamd::KernelRenderer::loadSpheres(scene_in, sp, al);
+            } else {
+                sp.resize(4 * (size_t)n);
+                al.resize((size_t)n);
+                rtamd::check(rt_generate_spheres((uint32_t)n, 0x2545F491u, sp.data(), al.data()));
+            }
+            if (!scene_out.empty()) rtamd::KernelRenderer::saveSpheres(scene_out, sp, al);
             rt_octree_params p;
             rt_octree_params_default(&p);
             p.max_depth = (uint32_t)depth;
             r.setScene(sp, al, &p);
             const rt_scene_info si = r.sceneInfo();
-            printf("scene: %u spheres, %u nodes, %u leaves, %u refs, depth %u/%u, build %.1f ms\n",
+            printf("scene: %u spheres, %u nodes, %u leaves, %u refs, depth %u/%u, %s build %.2f ms\n",
                    si.n_spheres, si.n_nodes, si.n_leaves, si.n_prim_refs, si.depth_reached,
-                   si.max_depth, si.build_ms);
+                   si.max_depth, si.builder == RT_BUILDER_HOST ? "host" : "device", si.build_ms);
         }
         rt_stats st{};
         double best = 1e30;

@@ -39,3 +39,20 @@ def test_cli_scene_runs(gpu):
                        timeout=120)
     assert r.returncode == 0, r.stderr
     assert "Mrays/s" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cli_scene_file_roundtrip_and_builders(gpu, tmp_path):
+    # generate -> save -> reload; device and host builders give the same image
+    f = tmp_path / "s.rtsph"
+    outs = []
+    for extra in (["--save-scene", str(f)], ["--scene", str(f)], ["--scene", str(f), "--host-build"]):
+        o = tmp_path / ("img%d.ppm" % len(outs))
+        r = subprocess.run([CLI, "--config", "c2", "--spheres", "3000", "--width", "160",
+                            "--height", "120", "--frames", "1", "--out", str(o), *extra],
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        assert ("host build" if "--host-build" in extra else "device build") in r.stdout
+        assert "3000 spheres" in r.stdout
+        outs.append(o.read_bytes())
+    assert outs[0] == outs[1] == outs[2]
