@@ -79,6 +79,9 @@ enum {
     RT_FLAG_NO_SHADOWS = 1u << 3,  /* skip shadow rays (Lambert without visibility) */
     RT_FLAG_HOST_BUILD = 1u << 4,  /* build the octree on the host (default: on the GPU);
                                       both builders produce the identical tree */
+    RT_FLAG_PROGRESSIVE = 1u << 5, /* scene mode: accumulate samples across frames while the
+                                      camera, size, scene and tile list stay unchanged; every
+                                      frame adds spp samples */
     /* bits 16..19: scene-kernel variant for A/B runs (0 = default = 1, one ray
      * per lane; 2 = 64-ray wave packets); images are identical */
     RT_FLAG_VARIANT_SHIFT = 16,
@@ -115,7 +118,7 @@ typedef struct rt_stats {
     uint64_t nodes_visited;  /* octree node records read (DESIGN.md counter definition) */
     uint64_t prims_tested;   /* ray-sphere tests                                        */
     float ms;                /* device time of the render launch(es), hipEvent          */
-    uint32_t reserved;
+    uint32_t samples_per_pixel; /* samples in the image: spp, or the accumulated total  */
 } rt_stats;
 
 typedef struct rt_scene_info {
@@ -216,6 +219,10 @@ int rt_render_tiles(rt_renderer* r, const uint32_t* tile_ids, uint32_t n_tiles,
 /* Scatter a packed tile buffer (layout above) into a W*H*4 device image. */
 int rt_unpack_tiles(rt_renderer* r, const void* dev_packed_rgba8, const uint32_t* tile_ids,
                     uint32_t n_tiles, uint32_t tile_size, void* dev_rgba8, void* stream);
+/* RT_FLAG_PROGRESSIVE: start the next frame from zero samples (any change of
+ * pose, intrinsic, size, scene or tile list does this by itself; setting the
+ * same pose again, as the reference's Displayer does every frame, does not). */
+int rt_reset_accumulation(rt_renderer* r);
 /* Wait for all work queued by this renderer. */
 int rt_synchronize(rt_renderer* r);
 /* Copy the internal framebuffer (and the float4 radiance buffer when

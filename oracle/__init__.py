@@ -49,6 +49,9 @@ def load() -> ctypes.CDLL:
         "orc_trace_brute": (ctypes.c_int, [_P, _P, _P, _f, _f, ctypes.c_int, _P, _P]),
         "orc_render_scene": (None, [_P, _u32, _u32, _P, _P, _u32, _u32, _u32, _P, _f, _u32, _u32,
                                     _u32, _u32, _u32, _u32, _P, _P, _P, ctypes.c_int]),
+        "orc_render_scene_frame": (None, [_P, _u32, _u32, _P, _P, _u32, _u32, _u32, _P, _f, _u32,
+                                          _u32, _u32, _u32, _u32, _u32, _u32, _P, _P, _P, _P,
+                                          ctypes.c_int]),
         "orc_max_threads": (ctypes.c_int, []),
     }
     for name, (res, args) in sig.items():
@@ -147,8 +150,10 @@ class Scene:
 
     def render(self, w, h, pose, K, spp=1, seed=0x2545F491, jitter=None, shadows=True,
                light_dir=(1.0, 1.0, -1.0), ambient=0.1, rect=None, row_step=1, row_phase=0,
-               n_threads=0, radiance=True):
-        """Returns (rgba8 (h,w,4), radiance (h,w,4) or None, counters[4])."""
+               n_threads=0, radiance=True, frame=0, accum=None):
+        """Returns (rgba8 (h,w,4), radiance (h,w,4) or None, counters[4]).
+        Progressive: pass accum (h,w,4) float32 running sums (updated in place)
+        and the frame index (0 starts over)."""
         if jitter is None:
             jitter = spp > 1
         flags = (1 if jitter else 0) | (0 if shadows else 8)
@@ -157,9 +162,12 @@ class Scene:
         out32 = np.zeros((h, w, 4), np.float32) if radiance else None
         cnt = np.zeros(4, np.uint64)
         pa, ka, la = _f32(pose, 16), _f32(K, 9), _f32(light_dir, 3)  # alive across the call
-        load().orc_render_scene(self._h, w, h, _p(pa), _p(ka), spp, seed,
-                                flags, _p(la), ambient, x0, y0, x1, y1,
-                                row_step, row_phase, _p(out8), _p(out32), _p(cnt), n_threads)
+        if accum is not None:
+            assert accum.dtype == np.float32 and accum.shape == (h, w, 4) and accum.flags.c_contiguous
+        load().orc_render_scene_frame(self._h, w, h, _p(pa), _p(ka), spp, seed,
+                                      flags, _p(la), ambient, x0, y0, x1, y1,
+                                      row_step, row_phase, frame, _p(accum), _p(out8), _p(out32),
+                                      _p(cnt), n_threads)
         return out8, out32, cnt
 
     def close(self):

@@ -611,6 +611,16 @@ void orc_render_scene(const orc_scene* s, uint32_t W, uint32_t H, const float po
                       const float light_dir[3], float ambient, uint32_t x0, uint32_t y0,
                       uint32_t x1, uint32_t y1, uint32_t row_step, uint32_t row_phase,
                       uint8_t* out8, float* out32, uint64_t counters[4], int n_threads) {
+    orc_render_scene_frame(s, W, H, pose, K, spp, seed, flags, light_dir, ambient, x0, y0, x1, y1,
+                           row_step, row_phase, 0, NULL, out8, out32, counters, n_threads);
+}
+
+void orc_render_scene_frame(const orc_scene* s, uint32_t W, uint32_t H, const float pose[16],
+                            const float K[9], uint32_t spp, uint32_t seed, uint32_t flags,
+                            const float light_dir[3], float ambient, uint32_t x0, uint32_t y0,
+                            uint32_t x1, uint32_t y1, uint32_t row_step, uint32_t row_phase,
+                            uint32_t frame, float* accum, uint8_t* out8, float* out32,
+                            uint64_t counters[4], int n_threads) {
     const float origin[3] = {pose[12], pose[13], pose[14]};
     const int jitter = (flags & 1u) != 0;
     const int shadows = (flags & 8u) == 0;
@@ -618,7 +628,10 @@ void orc_render_scene(const orc_scene* s, uint32_t W, uint32_t H, const float po
     const float ll = sqrtf(light_dir[0] * light_dir[0] + light_dir[1] * light_dir[1] +
                            light_dir[2] * light_dir[2]);
     const float L[3] = {-(light_dir[0] / ll), -(light_dir[1] / ll), -(light_dir[2] / ll)};
-    const float inv_spp = 1.0f / (float)spp;
+    /* progressive frame k (accum != NULL): samples [k*spp, (k+1)*spp), added
+     * onto the stored sums; the image is the mean over (k+1)*spp samples */
+    const uint32_t s_base = accum ? frame * spp : 0u;
+    const float inv_spp = 1.0f / (float)(accum ? (frame + 1u) * spp : spp);
     const float miss_r = 200.0f / 255.0f;
     const uint32_t seedmix = mix32(seed ^ 0x9E3779B9u);
     if (x1 > W) x1 = W;
@@ -649,9 +662,10 @@ void orc_render_scene(const orc_scene* s, uint32_t W, uint32_t H, const float po
             float ar = 0.0f, ag = 0.0f, ab = 0.0f;
             for (uint32_t sidx = 0; sidx < spp; ++sidx) {
                 float u = (float)x, v = (float)y;
+                const uint32_t sg = s_base + sidx;
                 if (jitter) {
-                    u = u + u01(mix32(hp ^ (sidx << 1)));
-                    v = v + u01(mix32(hp ^ ((sidx << 1) | 1u)));
+                    u = u + u01(mix32(hp ^ (sg << 1)));
+                    v = v + u01(mix32(hp ^ ((sg << 1) | 1u)));
                 }
                 float d[3];
                 orc_get_ray(pose, K, u, v, d);
@@ -698,16 +712,28 @@ void orc_render_scene(const orc_scene* s, uint32_t W, uint32_t H, const float po
                 if (slot == spw - 1 || sidx == spp - 1) {
                     const float tr = tree_sum(rbuf[0], g), tg = tree_sum(rbuf[1], g),
                                 tb = tree_sum(rbuf[2], g);
-                    if (sidx < spw) {
+                    if (sidx < spw && !(accum && frame)) {
                         ar = tr;
                         ag = tg;
                         ab = tb;
+                    } else if (sidx < spw) { /* progressive: onto the stored sum */
+                        const float* pa = accum + 4u * (size_t)pid;
+                        ar = pa[0] + tr;
+                        ag = pa[1] + tg;
+                        ab = pa[2] + tb;
                     } else {
                         ar = ar + tr;
                         ag = ag + tg;
                         ab = ab + tb;
                     }
                 }
+            }
+            if (accum) {
+                float* pa = accum + 4u * (size_t)pid;
+                pa[0] = ar;
+                pa[1] = ag;
+                pa[2] = ab;
+                pa[3] = 0.0f;
             }
             const float mr = ar * inv_spp, mg = ag * inv_spp, mb = ab * inv_spp;
             uint8_t* px = out8 + 4u * (size_t)pid;

@@ -65,6 +65,17 @@ void orc_render_scene(const orc_scene* s, uint32_t width, uint32_t height, const
                       uint32_t x1, uint32_t y1, uint32_t row_step, uint32_t row_phase,
                       uint8_t* out_rgba8, float* out_f32, uint64_t counters[4], int n_threads);
 
+/* Progressive frame `frame` (0, 1, ...) of RT_FLAG_PROGRESSIVE: samples
+ * [frame*spp, (frame+1)*spp) are added onto accum (W*H*4 running sums,
+ * in/out; ignored and zero-started at frame 0); the outputs are the mean over
+ * (frame+1)*spp samples.  accum == NULL is orc_render_scene. */
+void orc_render_scene_frame(const orc_scene* s, uint32_t width, uint32_t height,
+                            const float pose[16], const float K[9], uint32_t spp, uint32_t seed,
+                            uint32_t flags, const float light_dir[3], float ambient, uint32_t x0,
+                            uint32_t y0, uint32_t x1, uint32_t y1, uint32_t row_step,
+                            uint32_t row_phase, uint32_t frame, float* accum, uint8_t* out_rgba8,
+                            float* out_f32, uint64_t counters[4], int n_threads);
+
 int orc_max_threads(void);
 
 #ifdef __cplusplus

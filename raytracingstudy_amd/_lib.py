@@ -30,6 +30,7 @@ RT_FLAG_NO_JITTER = 1 << 1
 RT_FLAG_RADIANCE = 1 << 2
 RT_FLAG_NO_SHADOWS = 1 << 3
 RT_FLAG_HOST_BUILD = 1 << 4
+RT_FLAG_PROGRESSIVE = 1 << 5
 RT_BUILDER_DEVICE = 0
 RT_BUILDER_HOST = 1
 RT_FLAG_VARIANT_SHIFT = 16
@@ -71,11 +72,11 @@ class RtStats(ctypes.Structure):
         ("nodes_visited", ctypes.c_uint64),
         ("prims_tested", ctypes.c_uint64),
         ("ms", ctypes.c_float),
-        ("reserved", ctypes.c_uint32),
+        ("samples_per_pixel", ctypes.c_uint32),
     ]
 
     def as_dict(self) -> dict:
-        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+        return {f: getattr(self, f) for f, _ in self._fields_}
 
 
 class RtSceneInfo(ctypes.Structure):
@@ -132,6 +133,7 @@ SIGNATURES = {
     "rt_render": (_int, [_P, _P, _P, ctypes.POINTER(RtStats)]),
     "rt_render_tiles": (_int, [_P, _P, _u32, _u32, _P, _P, ctypes.POINTER(RtStats)]),
     "rt_unpack_tiles": (_int, [_P, _P, _P, _u32, _u32, _P, _P]),
+    "rt_reset_accumulation": (_int, [_P]),
     "rt_synchronize": (_int, [_P]),
     "rt_readback": (_int, [_P, _P, _P]),
     "rt_framebuffer": (_P, [_P]),

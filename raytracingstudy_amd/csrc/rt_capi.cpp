@@ -54,6 +54,9 @@ struct rt_renderer {
     uint32_t W = 0, H = 0;
     DevBuf<uint32_t> fb;
     DevBuf<float4> rad;
+    DevBuf<float4> accum;            // RT_FLAG_PROGRESSIVE running sums
+    uint32_t frames_accum = 0;       // frames in `accum` (0: next frame starts over)
+    uint64_t accum_sig = 0;          // which pixels the sums belong to (frame / tile list)
     DevBuf<unsigned long long> counters;
     DevBuf<uint32_t> tiles;          // tile list for rt_render_tiles
     std::vector<uint32_t> tiles_host;  // its host copy (source of the async upload)
@@ -140,6 +143,16 @@ void fill_frame_args(rt_renderer* r, FrameArgs& a) {
     a.L[2] = -(ld[2] / ll);
     a.ambient = r->cfg.ambient;
     a.inv_spp = 1.0f / static_cast<float>(a.spp);
+    if ((r->cfg.flags & RT_FLAG_PROGRESSIVE) && r->cfg.mode == RT_MODE_SCENE) {
+        // frame k traces samples [k*spp, (k+1)*spp) and adds them onto the
+        // stored sums: after K frames the image is the mean of K*spp samples
+        // (identical to one K*spp frame when spp is a multiple of 64)
+        if (uint64_t(r->frames_accum + 1) * a.spp >= (1ull << 31)) r->frames_accum = 0;
+        a.accum = r->accum.p;
+        a.s_base = r->frames_accum * a.spp;
+        a.accum_in = r->frames_accum ? 1u : 0u;
+        a.inv_spp = 1.0f / static_cast<float>((r->frames_accum + 1) * a.spp);
+    }
     a.counters = r->counters.p;
     a.sc.opt = (r->cfg.flags >> RT_FLAG_OPT_SHIFT) & 0xFu;
     const uint32_t v = (r->cfg.flags >> RT_FLAG_VARIANT_SHIFT) & 0xFu;
@@ -163,6 +176,7 @@ int build_scene(rt_renderer* r) {
     // any stream: the rebuild waits for the device
     RT_HIP(r, hipDeviceSynchronize());
     r->has_scene = false;
+    r->frames_accum = 0;
     rt_scene_info& in = r->info;
     const double upload_ms = in.upload_ms;
     in = rt_scene_info();
@@ -276,6 +290,19 @@ int upload_tiles(rt_renderer* r, DevBuf<uint32_t>& dev, std::vector<uint32_t>& h
     return RT_OK;
 }
 
+// Progressive sums belong to one pixel set: the full frame (sig 1) or one
+// tile list; rendering another set starts the accumulation over.
+void accum_pixels(rt_renderer* r, const uint32_t* ids, uint32_t n, uint32_t ts) {
+    uint64_t sig = 1;
+    if (ids) {
+        sig = 1469598103934665603ull ^ ts;
+        for (uint32_t i = 0; i < n; ++i) sig = (sig ^ ids[i]) * 1099511628211ull;
+        sig = (sig ^ n) * 1099511628211ull | 2u;
+    }
+    if (sig != r->accum_sig) r->frames_accum = 0;
+    r->accum_sig = sig;
+}
+
 int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : r->stream;
     if (r->cfg.mode == RT_MODE_SCENE && !r->has_scene)
@@ -285,6 +312,7 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     if (stats) RT_HIP(r, hipEventRecord(r->ev0, st));
     hipError_t e = r->cfg.mode == RT_MODE_SCENE ? launch_scene(a, st) : launch_compat(a, st);
     if (e != hipSuccess) return hip_fail(r, e, "kernel launch");
+    if (a.accum) ++r->frames_accum;
     if (stats) {
         RT_HIP(r, hipEventRecord(r->ev1, st));
         RT_HIP(r, hipEventSynchronize(r->ev1));
@@ -299,6 +327,8 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
         stats->nodes_visited = c[2];
         stats->prims_tested = c[3];
         stats->ms = ms;
+        stats->samples_per_pixel = r->cfg.mode != RT_MODE_SCENE ? 1u
+                                   : a.accum ? a.spp * r->frames_accum : a.spp;
     }
     return RT_OK;
 }
@@ -392,6 +422,13 @@ int rt_create(const rt_config* cfg, rt_renderer** out) {
         rt_destroy(r);
         return st;
     }
+    if (cfg->flags & RT_FLAG_PROGRESSIVE) {
+        if ((st = ensure(r, r->accum, (size_t)r->W * r->H))) {
+            g_last_error = r->err;
+            rt_destroy(r);
+            return st;
+        }
+    }
     if (cfg->flags & RT_FLAG_RADIANCE) {
         if ((st = ensure(r, r->rad, (size_t)r->W * r->H))) {
             g_last_error = r->err;
@@ -409,6 +446,7 @@ int rt_destroy(rt_renderer* r) {
     if (r->stream) (void)hipStreamSynchronize(r->stream);
     r->fb.release();
     r->rad.release();
+    r->accum.release();
     r->counters.release();
     r->tiles.release();
     r->utiles.release();
@@ -427,12 +465,14 @@ int rt_destroy(rt_renderer* r) {
 
 int rt_set_pose(rt_renderer* r, const float pose[16]) {
     if (!r || !pose) return fail(r, RT_E_INVALID, "rt_set_pose: null argument");
+    if (memcmp(r->pose, pose, sizeof(r->pose)) != 0) r->frames_accum = 0;
     memcpy(r->pose, pose, sizeof(r->pose));
     return RT_OK;
 }
 
 int rt_set_intrinsic(rt_renderer* r, const float K[9]) {
     if (!r || !K) return fail(r, RT_E_INVALID, "rt_set_intrinsic: null argument");
+    if (memcmp(r->K, K, sizeof(r->K)) != 0) r->frames_accum = 0;
     memcpy(r->K, K, sizeof(r->K));
     return RT_OK;
 }
@@ -453,7 +493,10 @@ int rt_resize(rt_renderer* r, uint32_t width, uint32_t height) {
     RT_HIP(r, hipStreamSynchronize(r->stream));
     r->W = width;
     r->H = height;
+    r->frames_accum = 0;
     if ((st = ensure(r, r->fb, (size_t)width * height))) return st;
+    if (r->cfg.flags & RT_FLAG_PROGRESSIVE)
+        if ((st = ensure(r, r->accum, (size_t)width * height))) return st;
     if (r->cfg.flags & RT_FLAG_RADIANCE)
         if ((st = ensure(r, r->rad, (size_t)width * height))) return st;
     rt_resize_intrinsic(width, height, r->K);
@@ -601,6 +644,7 @@ int rt_render(rt_renderer* r, void* dev_rgba8, void* stream, rt_stats* stats) {
     if (!r) return fail(r, RT_E_INVALID, "rt_render: null handle");
     int st;
     if ((st = set_device(r))) return st;
+    accum_pixels(r, nullptr, 0, 0);
     FrameArgs a;
     fill_frame_args(r, a);
     a.out8 = dev_rgba8 ? static_cast<uint32_t*>(dev_rgba8) : r->fb.p;
@@ -623,6 +667,7 @@ int rt_render_tiles(rt_renderer* r, const uint32_t* tile_ids, uint32_t n_tiles, 
         return RT_OK;
     }
     if ((st = upload_tiles(r, r->tiles, r->tiles_host, tile_ids, n_tiles, s))) return st;
+    accum_pixels(r, tile_ids, n_tiles, ts);
     FrameArgs a;
     fill_frame_args(r, a);
     a.out8 = static_cast<uint32_t*>(dev_packed);
@@ -658,6 +703,12 @@ int rt_unpack_tiles(rt_renderer* r, const void* dev_packed, const uint32_t* tile
     hipError_t e = launch_unpack(static_cast<const uint32_t*>(dev_packed), r->utiles.p, n_tiles, ts, tx,
                                  r->W, r->H, dev_rgba8 ? static_cast<uint32_t*>(dev_rgba8) : r->fb.p, s);
     if (e != hipSuccess) return hip_fail(r, e, "rt_unpack_tiles");
+    return RT_OK;
+}
+
+int rt_reset_accumulation(rt_renderer* r) {
+    if (!r) return fail(r, RT_E_INVALID, "rt_reset_accumulation: null handle");
+    r->frames_accum = 0;
     return RT_OK;
 }
 

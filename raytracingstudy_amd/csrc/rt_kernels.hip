@@ -753,13 +753,14 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
             for (uint32_t r = 0; r < a.rounds; ++r) {
                 const uint32_t s = r * spw + sub;
                 const bool valid = lane_pix && sub < spw && s < a.spp;
+                const uint32_t sg = a.s_base + s;  // sample index across accumulated frames
                 n_primary += valid ? 1u : 0u;
                 PixelOut c =
                     kVar == kVariantLaneUnified
-                        ? sample_color_unified<kChunk, kStats>(a, x, y, hp, s, valid, n_shadow,
+                        ? sample_color_unified<kChunk, kStats>(a, x, y, hp, sg, valid, n_shadow,
                                                                n_nodes, n_prims, stk)
-                        : sample_color<kVar, kChunk, kUni>(a, x, y, hp, s, valid, n_shadow, n_nodes,
-                                                           n_prims, stk);
+                        : sample_color<kVar, kChunk, kUni>(a, x, y, hp, sg, valid, n_shadow,
+                                                           n_nodes, n_prims, stk);
                 // Pixel sum of this round: pairwise butterfly over the pixel's g
                 // lanes (missing samples are 0) = oracle.c:tree_sum; rounds are
                 // then added in order in the leader's LDS slot.
@@ -770,8 +771,8 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
                     c.b += __shfl_xor(c.b, static_cast<int>(k), 64);
                 }
                 if (leader) {
-                    if (r) {
-                        const float4 A = acc[threadIdx.x];
+                    if (r || a.accum_in) {  // progressive: round 0 adds onto the stored sum
+                        const float4 A = r ? acc[threadIdx.x] : a.accum[pid];
                         c.r = A.x + c.r;
                         c.g = A.y + c.g;
                         c.b = A.z + c.b;
@@ -781,6 +782,7 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
             }
             if (leader) {
                 const float4 A = acc[threadIdx.x];
+                if (a.accum) a.accum[pid] = A;
                 const PixelOut p{A.x * a.inv_spp, A.y * a.inv_spp, A.z * a.inv_spp};
                 const uint32_t rgba = pack_rgba8(p);
                 if (kTiles) {

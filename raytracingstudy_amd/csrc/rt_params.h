@@ -71,7 +71,11 @@ struct FrameArgs {
     uint32_t shadows;
     float L[3];         // unit vector toward the light
     float ambient;
-    float inv_spp;
+    float inv_spp;      // 1 / samples in the image (all accumulated frames)
+    // progressive accumulation (RT_FLAG_PROGRESSIVE)
+    float4* accum;      // per-pixel running radiance sums (frame layout), or null
+    uint32_t s_base;    // first sample index of this frame (frame index * spp)
+    uint32_t accum_in;  // 1: add this frame's rounds onto the stored sums
     // output
     uint32_t* out8;     // RGBA8 (R in the low byte), frame- or tile-packed
     float4* out32;      // optional mean radiance (frame layout only), may be null

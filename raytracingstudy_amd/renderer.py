@@ -29,7 +29,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import (RT_FLAG_HOST_BUILD, RT_FLAG_JITTER, RT_FLAG_NO_JITTER, RT_FLAG_NO_SHADOWS,
-                   RT_FLAG_RADIANCE,
+                   RT_FLAG_PROGRESSIVE, RT_FLAG_RADIANCE,
                    RT_MODE_COMPAT, RT_MODE_SCENE, RtConfig, RtOctreeParams, RtSceneInfo,
                    RtStats, check)
 
@@ -105,7 +105,8 @@ class KernelRenderer:
                  seed: int = 0x2545F491, device: int = -1, jitter: Optional[bool] = None,
                  shadows: bool = True, radiance: bool = False,
                  light_dir: Sequence[float] = (1.0, 1.0, -1.0), ambient: float = 0.1,
-                 variant: int = 0, opt_off: int = 0, host_build: bool = False):
+                 variant: int = 0, opt_off: int = 0, host_build: bool = False,
+                 progressive: bool = False):
         lib = _lib.load()
         cfg = RtConfig()
         lib.rt_config_default(ctypes.byref(cfg))
@@ -125,6 +126,8 @@ class KernelRenderer:
             flags |= RT_FLAG_RADIANCE
         if host_build:
             flags |= RT_FLAG_HOST_BUILD
+        if progressive:
+            flags |= RT_FLAG_PROGRESSIVE
         flags |= (int(variant) & 0xF) << _lib.RT_FLAG_VARIANT_SHIFT
         flags |= (int(opt_off) & 0xF) << _lib.RT_FLAG_OPT_SHIFT
         cfg.flags = flags
@@ -243,6 +246,10 @@ class KernelRenderer:
                                         ids.shape[0], int(tile_size),
                                         ctypes.c_void_p(dev_rgba8) if dev_rgba8 else None,
                                         ctypes.c_void_p(stream) if stream else None), self._h)
+
+    def reset_accumulation(self) -> None:
+        """Progressive mode: the next frame starts from zero samples."""
+        check(self._lib.rt_reset_accumulation(self._h), self._h)
 
     def synchronize(self) -> None:
         check(self._lib.rt_synchronize(self._h), self._h)

@@ -98,7 +98,7 @@ def test_scene_from_device_memory(gpu):
     sp, al = rt.generate_spheres(5000, rt.SEED)
     dsp = torch.from_numpy(sp).cuda()
     dal = torch.from_numpy(al.view(np.int32)).cuda()
-    stream = torch.cuda.Stream()
+    stream = torch.cuda.current_stream()  # the stream that produced the tensors
     with _renderer() as ref, _renderer() as r:
         ref.set_scene(sp, al)
         ref.render()

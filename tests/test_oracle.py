@@ -181,3 +181,27 @@ def test_sample_hash_distribution(oracle):
     u = (v >> 8).astype(np.float64) / 2 ** 24
     assert len(np.unique(v)) == len(v)
     assert abs(u.mean() - 0.5) < 0.03
+
+
+def test_progressive_64spp_frames_equal_one_long_frame(oracle):
+    # SURVEY.md 8f F3 spec: K progressive frames of 64 spp add their round sums
+    # onto the stored sums in order, exactly as one 64*K-spp frame adds its rounds
+    import raytracingstudy_amd as rt
+    from raytracingstudy_amd.camera import scene_pose
+    sp, al = oracle.generate_spheres(1000, rt.SEED)
+    s = oracle.Scene(sp, al)
+    w, h = 12, 8
+    K = rt.resize_intrinsic(w, h).reshape(-1)
+    pose = scene_pose()
+    acc = np.zeros((h, w, 4), np.float32)
+    for k in range(3):
+        img, rad, _ = s.render(w, h, pose, K, spp=64, frame=k, accum=acc)
+    one, one_rad, _ = s.render(w, h, pose, K, spp=192)
+    assert np.array_equal(img, one) and np.array_equal(rad, one_rad)
+    assert np.allclose(acc[..., :3] / 192.0, one_rad[..., :3], rtol=1e-6)
+    # frame 0 ignores stale sums; small-spp frames still converge to a mean
+    acc[:] = 123.0
+    f0, _, _ = s.render(w, h, pose, K, spp=64, frame=0, accum=acc)
+    ref0, _, _ = s.render(w, h, pose, K, spp=64)
+    assert np.array_equal(f0, ref0)
+    s.close()
