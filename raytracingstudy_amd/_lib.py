@@ -162,6 +162,10 @@ def load() -> ctypes.CDLL:
                 " (or `make -C raytracingstudy_amd/csrc`); the render path has no CPU fallback")
         lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
         for name, (res, args) in SIGNATURES.items():
+            # an RT_AMD_LIB override (A/B against an older build) may predate
+            # some entry points; the in-tree library must export all of them
+            if os.environ.get("RT_AMD_LIB") and not hasattr(lib, name):
+                continue
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

@@ -702,7 +702,10 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
 // pixels, see launch_scene) are dealt to the 4 waves round-robin.  Neighbour
 // pixels run on one CU (L1 reuse) and the queue balances costly image regions.
 // kMinW = minimum waves per SIMD requested from the register allocator.
-template <bool kTiles, uint32_t kVar, int kMinW, int kChunk, bool kUni, bool kStats = true>
+// kProg: progressive frame (a.accum set); compiled separately so plain frames
+// keep their register budget.
+template <bool kTiles, uint32_t kVar, int kMinW, int kChunk, bool kUni, bool kStats = true,
+          bool kProg = false>
 __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     float4* acc = lds;  // [256] running pixel sums (leader lanes' slots)
@@ -750,10 +753,17 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
             const bool leader = lane_pix && sub == 0;
             const uint32_t pid = y * a.W + x;
             const uint32_t hp = mix32(a.seedmix ^ pid);
+            // progressive: the stored sum seeds the leader's LDS slot, so round 0
+            // adds onto it like any later round (nothing extra live in the walk)
+            if (kProg && a.accum_in && leader) acc[threadIdx.x] = a.accum[(size_t)y * a.W + x];
+            // sample index across accumulated frames: s_base + r*spw + sub
+            const uint32_t s_base = kProg ? a.s_base : 0u;
+            const uint32_t sub_base = s_base + sub;
+            const uint32_t s_end = s_base + a.spp;
+            const bool lane_ok = lane_pix && sub < spw;
             for (uint32_t r = 0; r < a.rounds; ++r) {
-                const uint32_t s = r * spw + sub;
-                const bool valid = lane_pix && sub < spw && s < a.spp;
-                const uint32_t sg = a.s_base + s;  // sample index across accumulated frames
+                const uint32_t sg = r * spw + sub_base;
+                const bool valid = lane_ok && sg < s_end;
                 n_primary += valid ? 1u : 0u;
                 PixelOut c =
                     kVar == kVariantLaneUnified
@@ -771,8 +781,8 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
                     c.b += __shfl_xor(c.b, static_cast<int>(k), 64);
                 }
                 if (leader) {
-                    if (r || a.accum_in) {  // progressive: round 0 adds onto the stored sum
-                        const float4 A = r ? acc[threadIdx.x] : a.accum[pid];
+                    if (r || (kProg && a.accum_in)) {
+                        const float4 A = acc[threadIdx.x];
                         c.r = A.x + c.r;
                         c.g = A.y + c.g;
                         c.b = A.z + c.b;
@@ -782,7 +792,7 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
             }
             if (leader) {
                 const float4 A = acc[threadIdx.x];
-                if (a.accum) a.accum[pid] = A;
+                if (kProg) a.accum[(size_t)y * a.W + x] = A;
                 const PixelOut p{A.x * a.inv_spp, A.y * a.inv_spp, A.z * a.inv_spp};
                 const uint32_t rgba = pack_rgba8(p);
                 if (kTiles) {
@@ -901,6 +911,15 @@ static void launch_persistent(K kernel, const FrameArgs& a_in, uint32_t, size_t 
 
 template <bool kTiles>
 static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStream_t st) {
+    if (a.accum) {  // progressive frames: the unified walk, whatever the A/B variant
+        if (a.count_work)
+            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true, true>, a,
+                              n_bt, lds, st);
+        else
+            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true>, a,
+                              n_bt, lds, st);
+        return;
+    }
     if (a.variant == kVariantLaneUnified1) {  // default: counters only in stats frames
         if (a.count_work)
             launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 1, false, true>, a, n_bt,
@@ -943,6 +962,7 @@ static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStr
 
 hipError_t launch_scene(const FrameArgs& a_in, hipStream_t st) {
     FrameArgs a = a_in;
+    if (a.accum) a.variant = kVariantLaneUnified;  // what launch_scene_t runs (LDS sizing)
     // wave mapping: spw samples x ppw pixels per wave (see scene_kernel)
     a.spw = a.spp >= 64u ? 64u : a.spp;
     a.g = 1;

@@ -49,6 +49,8 @@ def test_progressive_frames_match_oracle(gpu, oracle, spheres, spp):
 
 @pytest.mark.parametrize("variant", [0, 1, 2])
 def test_three_64spp_frames_equal_one_192spp_frame(gpu, spheres, variant):
+    # progressive frames always run the unified walk; the one-shot frame runs
+    # the requested variant (all variants give identical images)
     with _renderer(spheres, 64, variant=variant) as p, \
             _renderer(spheres, 192, progressive=False, variant=variant) as one:
         for _ in range(3):
