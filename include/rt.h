@@ -85,7 +85,7 @@ enum {
     /* bits 16..19: scene-kernel variant for A/B runs (0 = default = 1, one ray
      * per lane; 2 = 64-ray wave packets); images are identical */
     RT_FLAG_VARIANT_SHIFT = 16,
-    /* bits 20..23: A/B toggles that switch single optimisations off (0 = all on) */
+    /* bits 20..27: A/B toggles that switch single optimisations off or on (0 = defaults) */
     RT_FLAG_OPT_SHIFT = 20
 };
 

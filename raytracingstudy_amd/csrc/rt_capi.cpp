@@ -154,11 +154,14 @@ void fill_frame_args(rt_renderer* r, FrameArgs& a) {
         a.inv_spp = 1.0f / static_cast<float>((r->frames_accum + 1) * a.spp);
     }
     a.counters = r->counters.p;
-    a.sc.opt = (r->cfg.flags >> RT_FLAG_OPT_SHIFT) & 0xFu;
+    a.sc.opt = (r->cfg.flags >> RT_FLAG_OPT_SHIFT) & 0xFFu;
+    a.wq_chunk = 1u << ((a.sc.opt >> kOptChunkShift) & 3u);
     const uint32_t v = (r->cfg.flags >> RT_FLAG_VARIANT_SHIFT) & 0xFu;
-    // default: the counter-free unified walk for multi-sample frames, the
-    // counting one for 1-spp frames (faster there, tools/variants.py A/B)
-    a.variant = v ? v : (a.spp >= 8u ? kVariantLaneUnified2NoStats : kVariantLaneUnified);
+    // default: multi-sample frames are scheduled per wave over per-XCD queues
+    // (variant 13: C5 -15%, equal on C3, better on multi-GPU shares); 1-spp
+    // frames (8x8-pixel wave tiles) keep the block-tile queue (tools/variants.py A/B,
+    // profiles/r01/wave_queue_ab.log)
+    a.variant = v ? v : (a.spp >= 8u ? kVariantWaveQ : kVariantLaneUnified);
 }
 
 // Build the octree of the device sphere list (d_spheres) and point the

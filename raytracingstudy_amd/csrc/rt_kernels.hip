@@ -696,115 +696,185 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
     return c;
 }
 
-// Persistent workgroups pull 16x16-pixel block tiles from a device-wide
-// atomic queue (one returning atomic per tile; counters[kQueueSlot], zeroed
-// with the counters before every launch); the tile's wave tiles (tw x th
-// pixels, see launch_scene) are dealt to the 4 waves round-robin.  Neighbour
-// pixels run on one CU (L1 reuse) and the queue balances costly image regions.
+// Wave tile (tw x th pixels x spw samples, launch_scene) at pixel origin
+// (ox, oy); for a packed tile list also (k, olx, oly) = slot and tile-local
+// origin.  Rounds of spw samples, pairwise butterfly per round, rounds added
+// in order in the leader's LDS slot, then the mean is written.
+template <bool kTiles, uint32_t kVar, int kChunk, bool kUni, bool kStats, bool kProg>
+__device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc, void* stk,
+                                                uint32_t ox, uint32_t oy, uint32_t k,
+                                                uint32_t olx, uint32_t oly, uint32_t& n_primary,
+                                                uint32_t& n_shadow, uint32_t& n_nodes,
+                                                uint32_t& n_prims) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t spw = a.spw, g = a.g;
+    const uint32_t pix = lane / g, sub = lane & (g - 1u);
+    const uint32_t qx = pix % a.tw, qy = pix / a.tw;
+    const uint32_t x = ox + qx, y = oy + qy;
+    const bool lane_pix = pix < a.ppw && x < a.W && y < a.H;
+    const bool leader = lane_pix && sub == 0;
+    const uint32_t pid = y * a.W + x;
+    const uint32_t hp = mix32(a.seedmix ^ pid);
+    // progressive: the stored sum seeds the leader's LDS slot, so round 0
+    // adds onto it like any later round (nothing extra live in the walk)
+    if (kProg && a.accum_in && leader) acc[threadIdx.x] = a.accum[(size_t)y * a.W + x];
+    // sample index across accumulated frames: s_base + r*spw + sub
+    const uint32_t s_base = kProg ? a.s_base : 0u;
+    const uint32_t sub_base = s_base + sub;
+    const uint32_t s_end = s_base + a.spp;
+    const bool lane_ok = lane_pix && sub < spw;
+    for (uint32_t r = 0; r < a.rounds; ++r) {
+        const uint32_t sg = r * spw + sub_base;
+        const bool valid = lane_ok && sg < s_end;
+        n_primary += valid ? 1u : 0u;
+        PixelOut c = kVar == kVariantLaneUnified
+                         ? sample_color_unified<kChunk, kStats>(a, x, y, hp, sg, valid, n_shadow,
+                                                                n_nodes, n_prims, stk)
+                         : sample_color<kVar, kChunk, kUni>(a, x, y, hp, sg, valid, n_shadow,
+                                                            n_nodes, n_prims, stk);
+        // Pixel sum of this round: pairwise butterfly over the pixel's g
+        // lanes (missing samples are 0) = oracle.c:tree_sum; rounds are then
+        // added in order in the leader's LDS slot.
+        if (!valid) c = PixelOut{0.0f, 0.0f, 0.0f};
+        for (uint32_t m = 1; m < g; m <<= 1) {
+            c.r += __shfl_xor(c.r, static_cast<int>(m), 64);
+            c.g += __shfl_xor(c.g, static_cast<int>(m), 64);
+            c.b += __shfl_xor(c.b, static_cast<int>(m), 64);
+        }
+        if (leader) {
+            if (r || (kProg && a.accum_in)) {
+                const float4 A = acc[threadIdx.x];
+                c.r = A.x + c.r;
+                c.g = A.y + c.g;
+                c.b = A.z + c.b;
+            }
+            acc[threadIdx.x] = make_float4(c.r, c.g, c.b, 0.0f);
+        }
+    }
+    if (leader) {
+        const float4 A = acc[threadIdx.x];
+        if (kProg) a.accum[(size_t)y * a.W + x] = A;
+        const PixelOut p{A.x * a.inv_spp, A.y * a.inv_spp, A.z * a.inv_spp};
+        const uint32_t rgba = pack_rgba8(p);
+        if (kTiles) {
+            a.out8[(size_t)k * a.tile_size * a.tile_size + (oly + qy) * a.tile_size + olx + qx] = rgba;
+        } else {
+            a.out8[(size_t)y * a.W + x] = rgba;
+            if (a.out32) a.out32[(size_t)y * a.W + x] = make_float4(p.r, p.g, p.b, 1.0f);
+        }
+    } else if (kTiles && sub == 0 && pix < a.ppw) {
+        a.out8[(size_t)k * a.tile_size * a.tile_size + (oly + qy) * a.tile_size + olx + qx] =
+            0u;  // off-image pixel of an edge tile
+    }
+}
+
+// Work scheduling (persistent workgroups: grid = resident workgroups):
+//
+// kWaveQ = false: workgroups pull bts x bts block tiles from ONE device-wide
+//   queue head (a returning atomic per tile); the tile's wave tiles are dealt
+//   to the 4 waves round-robin, and the workgroup syncs per tile.
+// kWaveQ = true: every WAVE pulls single wave tiles on its own.  The wave
+//   tiles are numbered in 8x8 blocks (spatially coherent) and split into 8
+//   contiguous ranges, one per XCD group (blockIdx % 8: blocks dealt
+//   round-robin over the 8 XCDs share one, MI355X_MICROARCH.md "Workgroup
+//   dispatch"), each with its own head on its own cache line (one head
+//   saturates near 88 dequeues/us; per-XCD heads cost ~1.1 us under load).
+//   An XCD's waves work through its region (L2 locality), then steal from the
+//   next ranges.  No workgroup barrier; the tail is one wave tile.
+//
 // kMinW = minimum waves per SIMD requested from the register allocator.
 // kProg: progressive frame (a.accum set); compiled separately so plain frames
 // keep their register budget.
 template <bool kTiles, uint32_t kVar, int kMinW, int kChunk, bool kUni, bool kStats = true,
-          bool kProg = false>
+          bool kProg = false, bool kWaveQ = false>
 __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     float4* acc = lds;  // [256] running pixel sums (leader lanes' slots)
-    __shared__ uint32_t tile_slot;
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t wave = threadIdx.x >> 6;
     void* stk;
     if (kVar == kVariantPacket)
         stk = reinterpret_cast<PStackEntry*>(lds + kBlockThreads) + wave * a.stack_entries;
     else
         stk = reinterpret_cast<uint2*>(lds + kBlockThreads) + threadIdx.x;
-    const uint32_t spw = a.spw, g = a.g, tw = a.tw, th = a.th;
-    const uint32_t pix = lane / g, sub = lane & (g - 1u);
-    const uint32_t bts = a.bts;  // block-tile side (16, or 8/4 for small frames: launch_scene)
-    const uint32_t wtx = bts / tw, wtiles = wtx * (bts / th);
+    const uint32_t tw = a.tw, th = a.th;
     uint32_t n_shadow = 0, n_nodes = 0, n_prims = 0, n_primary = 0;
-    const uint32_t per_tile = kTiles ? (a.tile_size / bts) * (a.tile_size / bts) : 0u;
-    const uint32_t bx_n = (a.W + bts - 1) / bts;
-    const uint32_t n_bt = kTiles ? a.n_tiles * per_tile : bx_n * ((a.H + bts - 1) / bts);
-    for (;;) {
-        __syncthreads();  // every wave is done with the previous tile_slot
-        if (threadIdx.x == 0)
-            tile_slot = static_cast<uint32_t>(atomicAdd(a.counters + kQueueSlot, 1ull));
-        __syncthreads();
-        const uint32_t bt = tile_slot;
-        if (bt >= n_bt) break;
-        uint32_t ox, oy, k = 0, olx = 0, oly = 0;  // block-tile origin (frame / packed tile)
-        if (kTiles) {
-            const uint32_t tpr = a.tile_size / bts;
-            k = bt / per_tile;
-            const uint32_t b = bt - k * per_tile;
-            olx = (b % tpr) * bts;
-            oly = (b / tpr) * bts;
-            const uint32_t tile = a.tiles[k];
-            ox = (tile % a.tiles_x) * a.tile_size + olx;
-            oy = (tile / a.tiles_x) * a.tile_size + oly;
-        } else {
-            ox = (bt % bx_n) * bts;
-            oy = (bt / bx_n) * bts;
-        }
-        for (uint32_t wt = wave; wt < wtiles; wt += kBlockThreads / 64) {
-            const uint32_t qx = (wt % wtx) * tw + pix % tw;
-            const uint32_t qy = (wt / wtx) * th + pix / tw;
-            const uint32_t x = ox + qx, y = oy + qy;
-            const bool lane_pix = pix < a.ppw && x < a.W && y < a.H;
-            const bool leader = lane_pix && sub == 0;
-            const uint32_t pid = y * a.W + x;
-            const uint32_t hp = mix32(a.seedmix ^ pid);
-            // progressive: the stored sum seeds the leader's LDS slot, so round 0
-            // adds onto it like any later round (nothing extra live in the walk)
-            if (kProg && a.accum_in && leader) acc[threadIdx.x] = a.accum[(size_t)y * a.W + x];
-            // sample index across accumulated frames: s_base + r*spw + sub
-            const uint32_t s_base = kProg ? a.s_base : 0u;
-            const uint32_t sub_base = s_base + sub;
-            const uint32_t s_end = s_base + a.spp;
-            const bool lane_ok = lane_pix && sub < spw;
-            for (uint32_t r = 0; r < a.rounds; ++r) {
-                const uint32_t sg = r * spw + sub_base;
-                const bool valid = lane_ok && sg < s_end;
-                n_primary += valid ? 1u : 0u;
-                PixelOut c =
-                    kVar == kVariantLaneUnified
-                        ? sample_color_unified<kChunk, kStats>(a, x, y, hp, sg, valid, n_shadow,
-                                                               n_nodes, n_prims, stk)
-                        : sample_color<kVar, kChunk, kUni>(a, x, y, hp, sg, valid, n_shadow,
-                                                           n_nodes, n_prims, stk);
-                // Pixel sum of this round: pairwise butterfly over the pixel's g
-                // lanes (missing samples are 0) = oracle.c:tree_sum; rounds are
-                // then added in order in the leader's LDS slot.
-                if (!valid) c = PixelOut{0.0f, 0.0f, 0.0f};
-                for (uint32_t k = 1; k < g; k <<= 1) {
-                    c.r += __shfl_xor(c.r, static_cast<int>(k), 64);
-                    c.g += __shfl_xor(c.g, static_cast<int>(k), 64);
-                    c.b += __shfl_xor(c.b, static_cast<int>(k), 64);
+    if (kWaveQ) {
+        // wave-tile grid of the frame, or of one packed tile
+        const uint32_t gw = kTiles ? a.tile_size / tw : (a.W + tw - 1) / tw;
+        const uint32_t gh = kTiles ? a.tile_size / th : (a.H + th - 1) / th;
+        const uint32_t nbx = (gw + 7u) / 8u, nby = (gh + 7u) / 8u;
+        const uint32_t per_grid = nbx * nby * 64u;  // units incl. padding of edge blocks
+        const uint32_t n_units = kTiles ? a.n_tiles * per_grid : per_grid;
+        const uint32_t grp = blockIdx.x & 7u;
+        for (uint32_t hop = 0; hop < 8u; ++hop) {
+            const uint32_t q = (grp + hop) & 7u;
+            const uint32_t lo = static_cast<uint32_t>((uint64_t)n_units * q / 8u);
+            const uint32_t hi = static_cast<uint32_t>((uint64_t)n_units * (q + 1u) / 8u);
+            unsigned long long* head = a.counters + kWaveQueueBase + q * kWaveQueueStride;
+            const uint32_t chunk = a.wq_chunk;  // wave tiles per ticket
+            uint32_t u = hi, u_end = hi;
+            for (;;) {
+                if (u >= u_end) {  // take the next ticket
+                    uint32_t t = 0;
+                    if ((threadIdx.x & 63u) == 0) t = static_cast<uint32_t>(atomicAdd(head, 1ull));
+                    u = lo + __builtin_amdgcn_readfirstlane(t) * chunk;
+                    if (u >= hi) break;
+                    u_end = min(u + chunk, hi);
                 }
-                if (leader) {
-                    if (r || (kProg && a.accum_in)) {
-                        const float4 A = acc[threadIdx.x];
-                        c.r = A.x + c.r;
-                        c.g = A.y + c.g;
-                        c.b = A.z + c.b;
-                    }
-                    acc[threadIdx.x] = make_float4(c.r, c.g, c.b, 0.0f);
-                }
-            }
-            if (leader) {
-                const float4 A = acc[threadIdx.x];
-                if (kProg) a.accum[(size_t)y * a.W + x] = A;
-                const PixelOut p{A.x * a.inv_spp, A.y * a.inv_spp, A.z * a.inv_spp};
-                const uint32_t rgba = pack_rgba8(p);
+                const uint32_t cur = u++;
+                uint32_t k = 0, rem = cur;
                 if (kTiles) {
-                    a.out8[(size_t)k * a.tile_size * a.tile_size + (oly + qy) * a.tile_size + olx + qx] =
-                        rgba;
-                } else {
-                    a.out8[(size_t)y * a.W + x] = rgba;
-                    if (a.out32) a.out32[(size_t)y * a.W + x] = make_float4(p.r, p.g, p.b, 1.0f);
+                    k = cur / per_grid;
+                    rem = cur - k * per_grid;
                 }
-            } else if (kTiles && sub == 0 && pix < a.ppw) {
-                a.out8[(size_t)k * a.tile_size * a.tile_size + (oly + qy) * a.tile_size + olx + qx] =
-                    0u;  // off-image pixel of an edge tile
+                const uint32_t blk = rem >> 6, w = rem & 63u;
+                const uint32_t wx = (blk % nbx) * 8u + (w & 7u);
+                const uint32_t wy = (blk / nbx) * 8u + (w >> 3);
+                if (wx >= gw || wy >= gh) continue;  // padding of an edge block
+                const uint32_t olx = wx * tw, oly = wy * th;
+                uint32_t ox = olx, oy = oly;
+                if (kTiles) {
+                    const uint32_t tile = a.tiles[k];
+                    ox += (tile % a.tiles_x) * a.tile_size;
+                    oy += (tile / a.tiles_x) * a.tile_size;
+                }
+                shade_wave_tile<kTiles, kVar, kChunk, kUni, kStats, kProg>(
+                    a, acc, stk, ox, oy, k, olx, oly, n_primary, n_shadow, n_nodes, n_prims);
+            }
+        }
+    } else {
+        __shared__ uint32_t tile_slot;
+        const uint32_t bts = a.bts;  // block-tile side (16, or 8/4 for small frames)
+        const uint32_t wtx = bts / tw, wtiles = wtx * (bts / th);
+        const uint32_t per_tile = kTiles ? (a.tile_size / bts) * (a.tile_size / bts) : 0u;
+        const uint32_t bx_n = (a.W + bts - 1) / bts;
+        const uint32_t n_bt = kTiles ? a.n_tiles * per_tile : bx_n * ((a.H + bts - 1) / bts);
+        for (;;) {
+            __syncthreads();  // every wave is done with the previous tile_slot
+            if (threadIdx.x == 0)
+                tile_slot = static_cast<uint32_t>(atomicAdd(a.counters + kQueueSlot, 1ull));
+            __syncthreads();
+            const uint32_t bt = tile_slot;
+            if (bt >= n_bt) break;
+            uint32_t ox, oy, k = 0, olx = 0, oly = 0;  // block-tile origin (frame / packed tile)
+            if (kTiles) {
+                const uint32_t tpr = a.tile_size / bts;
+                k = bt / per_tile;
+                const uint32_t b = bt - k * per_tile;
+                olx = (b % tpr) * bts;
+                oly = (b / tpr) * bts;
+                const uint32_t tile = a.tiles[k];
+                ox = (tile % a.tiles_x) * a.tile_size + olx;
+                oy = (tile / a.tiles_x) * a.tile_size + oly;
+            } else {
+                ox = (bt % bx_n) * bts;
+                oy = (bt / bx_n) * bts;
+            }
+            for (uint32_t wt = wave; wt < wtiles; wt += kBlockThreads / 64) {
+                const uint32_t wox = (wt % wtx) * tw, woy = (wt / wtx) * th;
+                shade_wave_tile<kTiles, kVar, kChunk, kUni, kStats, kProg>(
+                    a, acc, stk, ox + wox, oy + woy, k, olx + wox, oly + woy, n_primary, n_shadow,
+                    n_nodes, n_prims);
             }
         }
     }
@@ -895,8 +965,9 @@ static uint32_t count_block_tiles(const FrameArgs& a, uint32_t b) {
 
 // Persistent launch: grid = resident workgroups; the block-tile side shrinks
 // (16 -> 8 -> 4 pixels, never below two wave tiles) until the tile queue holds
-// >= 4 tiles per resident workgroup, so a small frame (one rank's share of a
-// multi-GPU frame) still keeps every CU busy to the end.
+// >= 8 tiles per resident workgroup, so the dynamic queue can even out costly
+// image regions to the end (A/B, profiles/r01/bts_ab.log: 1080p 64 spp picks
+// 8x8 tiles, -6.4% vs 16x16; a 1/4 or 1/8 multi-GPU share picks 4x4).
 template <typename K>
 static void launch_persistent(K kernel, const FrameArgs& a_in, uint32_t, size_t lds,
                               hipStream_t st) {
@@ -904,20 +975,46 @@ static void launch_persistent(K kernel, const FrameArgs& a_in, uint32_t, size_t 
     const uint32_t res = resident_blocks(kernel, lds);
     const uint32_t min_side = 2u * std::max(a.tw, a.th);
     a.bts = kTileSide;
-    while (a.bts / 2u >= min_side && count_block_tiles(a, a.bts) < 4u * res) a.bts /= 2u;
+    const uint32_t force = (a.sc.opt >> kOptBtsShift) & 7u;
+    if (force && (kTileSide >> (force - 1u)) >= min_side)
+        a.bts = kTileSide >> (force - 1u);
+    else
+        while (a.bts / 2u >= min_side && count_block_tiles(a, a.bts) < 8u * res) a.bts /= 2u;
     const uint32_t grid = std::min(count_block_tiles(a, a.bts), res);
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlockThreads), lds, st, a);
+}
+
+// Per-wave queue launch: grid = resident workgroups, capped by the work.
+template <typename K>
+static void launch_waveq(K kernel, const FrameArgs& a, size_t lds, hipStream_t st) {
+    const uint32_t res = resident_blocks(kernel, lds);
+    uint64_t units;
+    if (a.tiles)
+        units = (uint64_t)a.n_tiles * (a.tile_size / a.tw) * (a.tile_size / a.th);
+    else
+        units = (uint64_t)((a.W + a.tw - 1) / a.tw) * ((a.H + a.th - 1) / a.th);
+    const uint64_t want = (units + kBlockThreads / 64 - 1) / (kBlockThreads / 64);
+    const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(res, want)));
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlockThreads), lds, st, a);
 }
 
 template <bool kTiles>
 static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStream_t st) {
     if (a.accum) {  // progressive frames: the unified walk, whatever the A/B variant
-        if (a.count_work)
+        if (a.spp >= 8u) {
+            if (a.count_work)
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true, true, true>,
+                             a, lds, st);
+            else
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true, true>,
+                             a, lds, st);
+        } else if (a.count_work) {
             launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true, true>, a,
                               n_bt, lds, st);
-        else
+        } else {
             launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true>, a,
                               n_bt, lds, st);
+        }
         return;
     }
     if (a.variant == kVariantLaneUnified1) {  // default: counters only in stats frames
@@ -945,6 +1042,14 @@ static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStr
         case kVariantLaneUnified1Stats:  // A/B only: variant 8 with the work counters compiled in
             launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 1, false, true>, a, n_bt,
                               lds, st);
+            break;
+        case kVariantWaveQ:  // per-wave scheduling over per-XCD queues
+            if (a.count_work)
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true, false, true>,
+                             a, lds, st);
+            else
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, false, true>,
+                             a, lds, st);
             break;
         case kVariantLaneUnified2NoStats:  // A/B only: variant 7 without the work counters
             if (a.count_work)

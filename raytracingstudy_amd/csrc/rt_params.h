@@ -23,13 +23,21 @@ constexpr uint32_t kVariantLaneUnified = 7;   // one walk instance for primary +
 constexpr uint32_t kVariantLaneUnified1 = 8;  // same, 1 in flight; counters only in stats frames
 constexpr uint32_t kVariantLaneUnified1Stats = 9;    // A/B: 8 with counters always compiled in
 constexpr uint32_t kVariantLaneUnified2NoStats = 10; // A/B: 7 with counters only in stats frames
+constexpr uint32_t kVariantWaveQ = 13;     // unified walk scheduled per wave over per-XCD queues
+                                           // (default for spp >= 8)
 
 // A/B toggles (rt_config.flags bits 20..23), results identical either way
 constexpr uint32_t kOptNoParentReuse = 1;  // always re-read the ancestor from the LDS stack
+constexpr uint32_t kOptBtsShift = 1;       // bits 1..3: force the block-tile side (A/B):
+                                           // 0 auto, 1 = 16, 2 = 8, 3 = 4, 4 = 2 pixels
+constexpr uint32_t kOptChunkShift = 4;     // bits 4..5: wave-queue tiles per ticket = 1 << k
 
-// counters[] layout: [0..3] stats, [kQueueSlot] tile queue head (own cache line)
+// counters[] layout: [0..3] stats, [kQueueSlot] block-tile queue head (own
+// cache line), then 8 per-XCD wave-queue heads, one per 128-byte line
 constexpr uint32_t kQueueSlot = 8;
-constexpr uint32_t kCounterWords = 16;
+constexpr uint32_t kWaveQueueBase = 16;
+constexpr uint32_t kWaveQueueStride = 16;
+constexpr uint32_t kCounterWords = kWaveQueueBase + 8 * kWaveQueueStride;
 
 // Pinhole camera (include/camera.h:9-56): K and R column-major like glm.
 struct CamArgs {
@@ -91,6 +99,7 @@ struct FrameArgs {
     uint32_t spw, g, ppw, tw, th, rounds;  // g = pow2ceil(spw) lanes per pixel
     uint32_t count_work;  // 1: also count node visits / sphere tests (stats frames)
     uint32_t bts;         // block-tile side in pixels (set by the launcher)
+    uint32_t wq_chunk;    // wave-queue scheduling: wave tiles per dequeue ticket
 };
 
 }  // namespace rtamd
