@@ -146,6 +146,64 @@ def test_scene_c3_rows_subsample(gpu, oracle, variant):
     assert np.array_equal(rad[rows], ref32[rows])
 
 
+@pytest.mark.parametrize("variant", [0, 10])
+def test_scene_c3_full_spp_rows(gpu, oracle, variant):
+    """C3 exactly as benchmarked (1920x1080, 64 spp, 100k spheres), every 64th row."""
+    img, rad, st, info, ref8, ref32, cnt, _ = _scene_pair(oracle, 100_000, 1920, 1080, 64,
+                                                           row_step=64, variant=variant)
+    rows = np.arange(0, 1080, 64)
+    assert np.array_equal(img[rows], ref8[rows])
+    assert np.array_equal(rad[rows], ref32[rows])
+
+
+def test_scene_c4_rows(gpu, oracle):
+    """C4 (3840x2160, 64 spp, 100k spheres), every 128th row."""
+    img, rad, st, info, ref8, ref32, cnt, _ = _scene_pair(oracle, 100_000, 3840, 2160, 64,
+                                                           row_step=128)
+    rows = np.arange(0, 2160, 128)
+    assert np.array_equal(img[rows], ref8[rows])
+    assert np.array_equal(rad[rows], ref32[rows])
+    assert st.primary_rays == 3840 * 2160 * 64
+
+
+def test_scene_c5_rows(gpu, oracle):
+    """C5 (1920x1080, 256 spp, 1M spheres, depth-12 octree), every 135th row."""
+    img, rad, st, info, ref8, ref32, cnt, oinfo = _scene_pair(oracle, 1_000_000, 1920, 1080, 256,
+                                                               depth=12, row_step=135)
+    assert (info["n_nodes"], info["n_prim_refs"]) == (oinfo["n_nodes"], oinfo["n_prim_refs"])
+    rows = np.arange(0, 1080, 135)
+    assert np.array_equal(img[rows], ref8[rows])
+    assert np.array_equal(rad[rows], ref32[rows])
+
+
+def test_c4_eight_rank_tile_plan(gpu):
+    """C4's multi-GPU plan on one GPU: 8 virtual ranks render their 64x64 tiles
+    (2040 tiles, last row 48 px) into packed slabs; unpacking every slab gives
+    the single-GPU frame byte for byte."""
+    import torch
+    w, h, ts, world = 3840, 2160, 64, 8
+    sp, al = rt.generate_spheres(100_000, rt.SEED)
+    with rt.KernelRenderer(w, h, mode="scene", spp=64) as r:
+        r.resize(w, h)
+        r.setPosition(scene_pose())
+        r.set_scene(sp, al)
+        r.render()
+        full = r.readback()
+        img = torch.zeros(w * h * 4, dtype=torch.uint8, device="cuda")
+        slab = torch.zeros(rt.tiles.slab_tiles(w, h, world, ts) * ts * ts * 4, dtype=torch.uint8,
+                           device="cuda")
+        torch.cuda.synchronize()
+        rays = 0
+        for k in range(world):
+            ids = rt.tiles.tiles_for_rank(w, h, k, world, ts)
+            st = r.render_tiles(ids, ts, slab.data_ptr(), stats=True)
+            rays += st.primary_rays
+            r.unpack_tiles(slab.data_ptr(), ids, ts, img.data_ptr())
+        r.synchronize()
+        assert rays == w * h * 64
+        assert np.array_equal(img.cpu().numpy().reshape(h, w, 4), full)
+
+
 def test_tiles_match_frame(gpu):
     import ctypes
     w, h, ts = 300, 200, 64
