@@ -157,7 +157,6 @@ void fill_frame_args(rt_renderer* r, FrameArgs& a) {
     a.counters = r->counters.p;
     a.sc.opt = (r->cfg.flags >> RT_FLAG_OPT_SHIFT) & 0xFFu;
     a.wq_chunk = 1u << ((a.sc.opt >> kOptChunkShift) & 3u);
-    a.sc.ktop = (a.sc.opt & kOptLdsTop) ? std::min<uint32_t>(r->info.n_nodes, kLdsTopNodes) : 0u;
     const uint32_t v = (r->cfg.flags >> RT_FLAG_VARIANT_SHIFT) & 0xFu;
     // default: multi-sample frames are scheduled per wave over per-XCD queues
     // (variant 13: C5 -15%, equal on C3, better on multi-GPU shares); 1-spp

@@ -271,9 +271,6 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 if (kUni) {
                     const uint32_t uslot = __builtin_amdgcn_readfirstlane(slot);
                     rec = __all(slot == uslot) ? nodes[uslot] : nodes[slot];
-                } else if (S.ktop) {  // breadth-first prefix staged in LDS (A/B)
-                    extern __shared__ __attribute__((aligned(16))) float4 lds_top[];
-                    rec = slot < S.ktop ? reinterpret_cast<const uint2*>(lds_top)[slot] : nodes[slot];
                 } else {
                     rec = nodes[slot];
                 }
@@ -308,7 +305,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             l1 = n1 & ~(size - 1u);
             l2 = n2 & ~(size - 1u);
             // m == 1: the ancestor is the node we are iterating (still in `node`)
-            if (m > 1 || (S.opt & kOptNoParentReuse)) node = depth ? stk[(depth - 1) * kBlockThreads] : S.root;
+            if (m > 1) node = depth ? stk[(depth - 1) * kBlockThreads] : S.root;
             t = texit;
         }
     }
@@ -792,20 +789,13 @@ template <bool kTiles, uint32_t kVar, int kMinW, int kChunk, bool kUni, bool kSt
           bool kProg = false, bool kWaveQ = false>
 __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
-    // LDS: [staged top node records][256 pixel sums][ancestor stacks]
-    const uint32_t top16 = (a.sc.ktop * 8u + 15u) / 16u;
-    if (a.sc.ktop) {
-        uint2* top = reinterpret_cast<uint2*>(lds);
-        for (uint32_t i = threadIdx.x; i < a.sc.ktop; i += kBlockThreads) top[i] = a.sc.nodes[i];
-        __syncthreads();
-    }
-    float4* acc = lds + top16;  // [256] running pixel sums (leader lanes' slots)
+    float4* acc = lds;  // [256] running pixel sums (leader lanes' slots)
     const uint32_t wave = threadIdx.x >> 6;
     void* stk;
     if (kVar == kVariantPacket)
-        stk = reinterpret_cast<PStackEntry*>(lds + top16 + kBlockThreads) + wave * a.stack_entries;
+        stk = reinterpret_cast<PStackEntry*>(lds + kBlockThreads) + wave * a.stack_entries;
     else
-        stk = reinterpret_cast<uint2*>(lds + top16 + kBlockThreads) + threadIdx.x;
+        stk = reinterpret_cast<uint2*>(lds + kBlockThreads) + threadIdx.x;
     const uint32_t tw = a.tw, th = a.th;
     uint32_t n_shadow = 0, n_nodes = 0, n_prims = 0, n_primary = 0;
     if (kWaveQ) {
@@ -927,8 +917,7 @@ hipError_t launch_compat(const FrameArgs& a, hipStream_t st) {
 }
 
 size_t scene_lds_bytes(const FrameArgs& a) {
-    const size_t colours = kBlockThreads * sizeof(float4) +   // pixel sums
-                           (a.sc.ktop * 8u + 15u) / 16u * 16u;  // staged top nodes
+    const size_t colours = kBlockThreads * sizeof(float4);  // pixel sums
     if (a.variant == kVariantPacket)
         return colours + static_cast<size_t>(a.stack_entries) * (kBlockThreads / 64) * sizeof(PStackEntry);
     const uint32_t levels = a.sc.max_depth > 1 ? a.sc.max_depth - 1 : 1;

@@ -27,12 +27,9 @@ constexpr uint32_t kVariantWaveQ = 13;     // unified walk scheduled per wave ov
                                            // (default for spp >= 8)
 
 // A/B toggles (rt_config.flags bits 20..23), results identical either way
-constexpr uint32_t kOptNoParentReuse = 1;  // always re-read the ancestor from the LDS stack
 constexpr uint32_t kOptBtsShift = 1;       // bits 1..3: force the block-tile side (A/B):
                                            // 0 auto, 1 = 16, 2 = 8, 3 = 4, 4 = 2 pixels
 constexpr uint32_t kOptChunkShift = 4;     // bits 4..5: wave-queue tiles per ticket = 1 << k
-constexpr uint32_t kOptLdsTop = 64;        // bit 6: stage the first kLdsTopNodes records in LDS
-constexpr uint32_t kLdsTopNodes = 1024;
 
 // counters[] layout: [0..3] stats, [kQueueSlot] block-tile queue head (own
 // cache line), then 8 per-XCD wave-queue heads, one per 128-byte line
@@ -69,7 +66,6 @@ struct SceneArgs {
     float scale[3];          // G / (rmax - rmin), f32
     float G;
     uint32_t opt;            // kOpt* toggles (A/B only; 0 = all optimisations on)
-    uint32_t ktop;           // node records staged in LDS (breadth-first prefix), 0 = none
 };
 
 struct FrameArgs {
