@@ -48,6 +48,11 @@ def parse():
     ap.add_argument("--tiles", action="store_true",
                     help="use the multi-GPU tile path (render_tiles + gather + unpack) even at N=1, "
                          "and check the frame against a whole-frame render")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="process-group backend for N>1 (nccl = RCCL; gloo only to rehearse "
+                         "the multi-rank path on one GPU)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal: every rank uses cuda:0 (with --backend gloo)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="PMC traffic summary written by tools/pmc_traffic.py")
     return ap.parse_args()
@@ -95,9 +100,16 @@ def main():
     from raytracingstudy_amd.camera import scene_pose
     from raytracingstudy_amd.dist import TileSharder
 
+    if args.same_device:
+        if args.backend != "gloo":
+            raise SystemExit("--same-device is a gloo rehearsal (RCCL needs one GPU per rank)")
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     cfg = rt.CONFIGS[args.config]
     if cfg.mode != "scene":
         raise SystemExit("bench runs a scene config (c2..c5)")
@@ -176,8 +188,9 @@ def main():
     elapsed = time.perf_counter() - t0
 
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else float("nan")
-    el_t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    tot = cnt.clone()
+    red_dev = dev if args.backend == "nccl" else torch.device("cpu")
+    el_t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
+    tot = cnt.clone().to(red_dev)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)

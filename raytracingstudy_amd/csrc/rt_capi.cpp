@@ -59,10 +59,16 @@ struct rt_renderer {
     uint32_t frames_accum = 0;       // frames in `accum` (0: next frame starts over)
     uint64_t accum_sig = 0;          // which pixels the sums belong to (frame / tile list)
     DevBuf<unsigned long long> counters;
-    DevBuf<uint32_t> tiles;          // tile list for rt_render_tiles
-    std::vector<uint32_t> tiles_host;  // its host copy (source of the async upload)
-    DevBuf<uint32_t> utiles;         // tile list for rt_unpack_tiles
-    std::vector<uint32_t> utiles_host;
+    // device copies of recently used tile lists (rt_render_tiles: this rank's
+    // list; rt_unpack_tiles on rank 0: one list per peer), least recently used
+    // evicted; each host vector stays alive as the source of its async upload
+    struct TileList {
+        std::vector<uint32_t> host;
+        DevBuf<uint32_t> dev;
+        uint64_t used = 0;
+    };
+    std::vector<TileList> tile_lists;
+    uint64_t tile_clock = 0;
     // scene: the sphere list lives in d_spheres/d_albedo; `spheres` is a host
     // copy when the scene came from host memory (host builder input)
     uint32_t n_spheres = 0;
@@ -281,16 +287,37 @@ int check_tiles(rt_renderer* r, const uint32_t* ids, uint32_t n_tiles, uint32_t 
     return RT_OK;
 }
 
-// Upload a tile list only when it changed; the host vector stays alive as the
-// source of the asynchronous copy, so steady-state frames never synchronise.
-int upload_tiles(rt_renderer* r, DevBuf<uint32_t>& dev, std::vector<uint32_t>& host,
-                 const uint32_t* ids, uint32_t n, hipStream_t s) {
-    if (host.size() == n && dev.p && memcmp(host.data(), ids, n * sizeof(uint32_t)) == 0)
-        return RT_OK;
-    int st;
-    if ((st = ensure(r, dev, n))) return st;
-    host.assign(ids, ids + n);
-    RT_HIP(r, hipMemcpyAsync(dev.p, host.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+// Device copy of a tile list: found in the cache when the same list was used
+// recently (steady-state frames never copy or synchronise), else uploaded
+// asynchronously into the least recently used slot.
+constexpr size_t kTileListSlots = 16;
+
+int tile_list(rt_renderer* r, const uint32_t* ids, uint32_t n, hipStream_t s, const uint32_t** out) {
+    rt_renderer::TileList* hit = nullptr;
+    for (auto& e : r->tile_lists)
+        if (e.host.size() == n && e.dev.p && memcmp(e.host.data(), ids, n * sizeof(uint32_t)) == 0) {
+            hit = &e;
+            break;
+        }
+    if (!hit) {
+        if (r->tile_lists.size() < kTileListSlots) {
+            r->tile_lists.emplace_back();
+            hit = &r->tile_lists.back();
+        } else {
+            hit = &r->tile_lists[0];
+            for (auto& e : r->tile_lists)
+                if (e.used < hit->used) hit = &e;
+            // its previous upload may still be in flight on some stream
+            RT_HIP(r, hipDeviceSynchronize());
+        }
+        int st;
+        if ((st = ensure(r, hit->dev, n))) return st;
+        hit->host.assign(ids, ids + n);
+        RT_HIP(r, hipMemcpyAsync(hit->dev.p, hit->host.data(), n * sizeof(uint32_t),
+                                 hipMemcpyHostToDevice, s));
+    }
+    hit->used = ++r->tile_clock;
+    *out = hit->dev.p;
     return RT_OK;
 }
 
@@ -452,8 +479,7 @@ int rt_destroy(rt_renderer* r) {
     r->rad.release();
     r->accum.release();
     r->counters.release();
-    r->tiles.release();
-    r->utiles.release();
+    for (auto& e : r->tile_lists) e.dev.release();
     r->d_nodes.release();
     r->d_prim_sp.release();
     r->d_prim_idx.release();
@@ -670,13 +696,14 @@ int rt_render_tiles(rt_renderer* r, const uint32_t* tile_ids, uint32_t n_tiles, 
         if (stats) memset(stats, 0, sizeof(*stats));
         return RT_OK;
     }
-    if ((st = upload_tiles(r, r->tiles, r->tiles_host, tile_ids, n_tiles, s))) return st;
+    const uint32_t* dev_ids = nullptr;
+    if ((st = tile_list(r, tile_ids, n_tiles, s, &dev_ids))) return st;
     accum_pixels(r, tile_ids, n_tiles, ts);
     FrameArgs a;
     fill_frame_args(r, a);
     a.out8 = static_cast<uint32_t*>(dev_packed);
     a.out32 = nullptr;
-    a.tiles = r->tiles.p;
+    a.tiles = dev_ids;
     a.n_tiles = n_tiles;
     a.tile_size = ts;
     a.tiles_x = tx;
@@ -703,8 +730,9 @@ int rt_unpack_tiles(rt_renderer* r, const void* dev_packed, const uint32_t* tile
     const uint32_t tx = (r->W + ts - 1) / ts;
     if ((st = set_device(r))) return st;
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->stream;
-    if ((st = upload_tiles(r, r->utiles, r->utiles_host, tile_ids, n_tiles, s))) return st;
-    hipError_t e = launch_unpack(static_cast<const uint32_t*>(dev_packed), r->utiles.p, n_tiles, ts, tx,
+    const uint32_t* dev_ids = nullptr;
+    if ((st = tile_list(r, tile_ids, n_tiles, s, &dev_ids))) return st;
+    hipError_t e = launch_unpack(static_cast<const uint32_t*>(dev_packed), dev_ids, n_tiles, ts, tx,
                                  r->W, r->H, dev_rgba8 ? static_cast<uint32_t*>(dev_rgba8) : r->fb.p, s);
     if (e != hipSuccess) return hip_fail(r, e, "rt_unpack_tiles");
     return RT_OK;

@@ -285,8 +285,9 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             const float e0 = plane(0, l0 + size);
             const float e1 = plane(1, l1 + size);
             const float e2 = plane(2, l2 + size);
-            float texit = e0 < e1 ? e0 : e1;
-            texit = texit < e2 ? texit : e2;
+            // one v_min3_f32 (the oracle's ternaries can differ only in the sign
+            // of a zero, and texit is only ever compared: identical walks)
+            const float texit = fminf(fminf(e0, e1), e2);
             if (!kAnyHit && best_t < texit) break;
             if (texit >= t1) break;
             // step every axis whose exit plane is texit; the flipped bits give the

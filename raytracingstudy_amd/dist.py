@@ -46,14 +46,20 @@ class TileSharder:
             return [slab]
         import torch
         import torch.distributed as dist
+        # gloo moves host tensors only: device slabs are staged through host
+        # memory (rehearsal of the multi-rank path; RCCL gathers device slabs)
+        staged = slab.is_cuda and dist.get_backend(group) == "gloo"
+        src = slab.cpu() if staged else slab
         out = None
         if self.rank == 0:
-            key = (tuple(slab.shape), slab.dtype, slab.device)
+            key = (tuple(src.shape), src.dtype, src.device)
             if getattr(self, "_recv_key", None) != key:
-                self._recv = [torch.empty_like(slab) for _ in range(self.world)]
+                self._recv = [torch.empty_like(src) for _ in range(self.world)]
                 self._recv_key = key
             out = self._recv
-        dist.gather(slab, out, dst=0, group=group)
+        dist.gather(src, out, dst=0, group=group)
+        if staged and out is not None:
+            out = [t.to(slab.device) for t in out]
         return out
 
     def unpack(self, gathered, unpack_fn: Callable[[object, np.ndarray], None]) -> None:
