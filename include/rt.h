@@ -210,6 +210,14 @@ int rt_load_spheres(const char* path, float* spheres_out, uint32_t* albedo_out,
  * stream: a hipStream_t or NULL (the renderer's own stream).  Asynchronous
  * unless stats != NULL (then it waits for the frame and fills the counters). */
 int rt_render(rt_renderer* r, void* dev_rgba8, void* stream, rt_stats* stats);
+/* GL interop.  The Displayer registers its PBO with
+ * hipGraphicsGLRegisterBuffer (where it called cudaGraphicsGLRegisterBuffer,
+ * src/window/displayer.cpp:13-17, and again after a resize, :61-70) and binds
+ * the resource here.  Then rt_render(r, NULL, stream, stats) maps it, renders
+ * into the mapped pointer and unmaps it: the reference's render()
+ * (src/renderer.cu:145-151).  NULL unbinds (render into the internal
+ * framebuffer).  The resource stays owned by the caller. */
+int rt_bind_graphics_resource(rt_renderer* r, void* hip_graphics_resource);
 /* Render only the listed image tiles (tile_size x tile_size, row-major tile
  * ids over ceil(W/ts) x ceil(H/ts)) into a packed device buffer of
  * n_tiles*ts*ts*4 bytes: tile k's pixel (lx,ly) at byte 4*(k*ts*ts + ly*ts + lx);

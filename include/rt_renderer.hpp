@@ -48,6 +48,14 @@ public:
         cfg.device = device;
         check(rt_create(&cfg, &r_));
     }
+    // The reference's exact constructor shape (src/renderer.cu:124-141): the
+    // PBO resource (registered with hipGraphicsGLRegisterBuffer) is bound, so
+    // render() maps, renders into and unmaps it.
+    KernelRenderer(void* graphics_resource, int width, int height, uint32_t mode = RT_MODE_COMPAT,
+                   uint32_t spp = 1)
+        : KernelRenderer(width, height, mode, spp) {
+        setGraphicsResource(graphics_resource);
+    }
     explicit KernelRenderer(const rt_config& cfg) { check(rt_create(&cfg, &r_)); }
     ~KernelRenderer() { rt_destroy(r_); }
     KernelRenderer(const KernelRenderer&) = delete;
@@ -56,6 +64,11 @@ public:
     // render() (src/renderer.cu:143-153): dev_rgba8 = mapped PBO pointer.
     void render(void* dev_rgba8 = nullptr, void* stream = nullptr, rt_stats* stats = nullptr) {
         check(rt_render(r_, dev_rgba8, stream, stats), r_);
+    }
+    // the reference assigns renderer->cudaResource after re-registering the
+    // resized PBO (src/window/displayer.cpp:61-70)
+    void setGraphicsResource(void* graphics_resource) {
+        check(rt_bind_graphics_resource(r_, graphics_resource), r_);
     }
     // resize(int, int) (src/renderer.cu:155-187)
     void resize(int width, int height) {

@@ -131,6 +131,7 @@ SIGNATURES = {
     "rt_load_spheres": (_int, [ctypes.c_char_p, _P, _P, _u32, ctypes.POINTER(_u32)]),
     "rt_generate_spheres": (_int, [_u32, _u32, _P, _P]),
     "rt_render": (_int, [_P, _P, _P, ctypes.POINTER(RtStats)]),
+    "rt_bind_graphics_resource": (_int, [_P, _P]),
     "rt_render_tiles": (_int, [_P, _P, _u32, _u32, _P, _P, ctypes.POINTER(RtStats)]),
     "rt_unpack_tiles": (_int, [_P, _P, _P, _u32, _u32, _P, _P]),
     "rt_reset_accumulation": (_int, [_P]),

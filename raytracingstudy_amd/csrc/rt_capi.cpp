@@ -69,6 +69,8 @@ struct rt_renderer {
     };
     std::vector<TileList> tile_lists;
     uint64_t tile_clock = 0;
+    // GL interop: the Displayer's registered PBO (hipGraphicsGLRegisterBuffer)
+    hipGraphicsResource_t gfx = nullptr;
     // scene: the sphere list lives in d_spheres/d_albedo; `spheres` is a host
     // copy when the scene came from host memory (host builder input)
     uint32_t n_spheres = 0;
@@ -679,7 +681,34 @@ int rt_render(rt_renderer* r, void* dev_rgba8, void* stream, rt_stats* stats) {
     fill_frame_args(r, a);
     a.out8 = dev_rgba8 ? static_cast<uint32_t*>(dev_rgba8) : r->fb.p;
     a.out32 = (r->cfg.flags & RT_FLAG_RADIANCE) ? r->rad.p : nullptr;
-    return do_render(r, a, stream, stats);
+    if (dev_rgba8 || !r->gfx) return do_render(r, a, stream, stats);
+    // the reference's render(): map the PBO, launch into it, unmap
+    // (src/renderer.cu:145-151)
+    hipStream_t hs = stream ? static_cast<hipStream_t>(stream) : r->stream;
+    RT_HIP(r, hipGraphicsMapResources(1, &r->gfx, hs));
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    hipError_t e = hipGraphicsResourceGetMappedPointer(&ptr, &bytes, r->gfx);
+    if (e == hipSuccess && bytes < (size_t)r->W * r->H * 4) {
+        (void)hipGraphicsUnmapResources(1, &r->gfx, hs);
+        return fail(r, RT_E_INVALID, "rt_render: bound graphics resource smaller than W*H*4 bytes");
+    }
+    if (e != hipSuccess) {
+        (void)hipGraphicsUnmapResources(1, &r->gfx, hs);
+        return hip_fail(r, e, "hipGraphicsResourceGetMappedPointer");
+    }
+    a.out8 = static_cast<uint32_t*>(ptr);
+    st = do_render(r, a, hs, stats);
+    hipError_t eu = hipGraphicsUnmapResources(1, &r->gfx, hs);
+    if (st) return st;
+    if (eu != hipSuccess) return hip_fail(r, eu, "hipGraphicsUnmapResources");
+    return RT_OK;
+}
+
+int rt_bind_graphics_resource(rt_renderer* r, void* resource) {
+    if (!r) return fail(r, RT_E_INVALID, "rt_bind_graphics_resource: null handle");
+    r->gfx = static_cast<hipGraphicsResource_t>(resource);
+    return RT_OK;
 }
 
 int rt_render_tiles(rt_renderer* r, const uint32_t* tile_ids, uint32_t n_tiles, uint32_t ts,

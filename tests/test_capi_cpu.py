@@ -114,3 +114,18 @@ def test_product_never_imports_oracle():
                 src = open(os.path.join(dp, f)).read()
                 assert "import oracle" not in src and "liboracle" not in src, f
                 assert "orc_" not in src, f
+
+
+def test_gl_interop_header_compiles(tmp_path):
+    """the Displayer-side PBO registration (include/rt_gl.hpp)
+    and the resource-taking KernelRenderer compile against the GL and HIP headers."""
+    import shutil
+    import subprocess
+    if not os.path.exists("/usr/include/GL/gl.h"):
+        pytest.skip("no GL headers in this image")
+    cxx = shutil.which("g++")
+    r = subprocess.run([cxx, "-std=c++17", "-fsyntax-only", "-D__HIP_PLATFORM_AMD__",
+                        "-I/opt/rocm/include", "-I" + os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "tests", "native", "gl_interop_use.cpp")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

@@ -319,3 +319,28 @@ def test_errors_are_loud(gpu):
             r.render_tiles([0], 48, 0)  # tile size not a multiple of 64
         with pytest.raises(rt._lib.RtError):
             r.readback_radiance()  # no RT_FLAG_RADIANCE
+
+
+def test_graphics_resource_binding_plumbing(gpu):
+    """F2 plumbing (a GL context cannot be created on the GPU box): binding NULL
+    keeps rendering into the internal framebuffer; an explicit device pointer
+    always wins over a bound resource."""
+    import ctypes
+    import torch
+    sp, al = rt.generate_spheres(1000, rt.SEED)
+    with rt.KernelRenderer(64, 48, mode="scene", spp=2) as r:
+        r.resize(64, 48)
+        r.setPosition(scene_pose())
+        r.set_scene(sp, al)
+        r.render()
+        ref = r.readback()
+        lib = rt._lib.load()
+        assert lib.rt_bind_graphics_resource(r._h, None) == 0
+        r.render()
+        assert np.array_equal(r.readback(), ref)
+        buf = torch.zeros(64 * 48 * 4, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        r.render(buf.data_ptr())
+        r.synchronize()
+        assert np.array_equal(buf.cpu().numpy().reshape(48, 64, 4), ref)
+    assert lib.rt_bind_graphics_resource(None, None) == rt._lib.RT_E_INVALID
