@@ -81,9 +81,18 @@ def cpu_baseline(cfg, K, pose, target_s: float) -> dict:
     el = time.perf_counter() - t
     rays = int(c[0]) + int(c[1])
     n_rows = len(range(step // 2, cfg.height, step))
+    # also one core, on 16 evenly spaced rows
+    s1 = max(1, cfg.height // 16)
+    t = time.perf_counter()
+    _, _, c1 = sc.render(cfg.width, cfg.height, pose, K, spp=cfg.spp, row_step=s1, row_phase=s1 // 2,
+                         n_threads=1, radiance=False)
+    el1 = time.perf_counter() - t
+    rays1 = int(c1[0]) + int(c1[1])
     return {"value": round(rays / el / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{cfg.name} scene, every {step}th row ({n_rows} rows x {cfg.width} px x "
-                      f"{cfg.spp} spp = {int(c[0])} primary + {int(c[1])} shadow rays) in {el:.1f} s"}
+                      f"{cfg.spp} spp = {int(c[0])} primary + {int(c[1])} shadow rays) in {el:.1f} s",
+            "single_core": {"value": round(rays1 / el1 / 1e6, 3), "unit": "Mrays/s", "cores": 1,
+                            "sample": f"every {s1}th row ({rays1} rays) in {el1:.2f} s"}}
 
 
 def main():
