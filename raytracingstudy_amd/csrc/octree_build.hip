@@ -24,6 +24,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "octree_gpu.h"
+#include "rt_params.h"
 
 namespace rtamd {
 namespace {
@@ -491,7 +492,8 @@ hipError_t GpuOctreeBuilder::build(const float4* sp, uint32_t n, const float cfg
         R = t.w;
         cur = nxt;
     }
-    RT_TRY(reserve(prim_sp_b_, std::max<uint32_t>(prim_total, 1), 0, st));
+    // + kPrimPad: the scalar leaf path may read up to 3 spheres past a leaf's end
+    RT_TRY(reserve(prim_sp_b_, size_t(prim_total) + kPrimPad, 0, st));
     if (prim_total) {
         hipLaunchKernelGGL(gather_prims, dim3(blocks_for(prim_total)), dim3(kThreads), 0, st, sp,
                            prim_idx_b_.p, prim_total, prim_sp_b_.p);

@@ -208,7 +208,7 @@ int build_scene(rt_renderer* r) {
         build_octree(r->spheres.data(), n, p.min, p.max, depth, cap, tree);
         const size_t nn = tree.nodes.size(), np = tree.prim_idx.size();
         if ((st = ensure(r, r->d_nodes, nn))) return st;
-        if ((st = ensure(r, r->d_prim_sp, np))) return st;
+        if ((st = ensure(r, r->d_prim_sp, np + kPrimPad))) return st;  // scalar-read padding
         if ((st = ensure(r, r->d_prim_idx, np))) return st;
         RT_HIP(r, hipMemcpy(r->d_nodes.p, tree.nodes.data(), nn * sizeof(uint2),
                             hipMemcpyHostToDevice));

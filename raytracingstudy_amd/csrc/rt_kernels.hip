@@ -142,11 +142,12 @@ __device__ __forceinline__ bool isect(float o0, float o1, float o2, float d0, fl
 // kAnyHit: compile-time any-hit; with kDynAny the mode comes from `any_rt`
 // instead, so ONE inlined walk serves both the primary and the shadow ray.
 template <bool kAnyHitT, int kChunk = 4, bool kUni = false, bool kDynAny = false,
-          bool kStats = true>
+          bool kStats = true, bool kLdsLeaf = false, bool kSmemLeaf = false>
 __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, float o2, float d0,
                                      float d1, float d2, float tmin, float tmax, float& tout,
                                      uint32_t& iout, uint32_t& n_nodes, uint32_t& n_prims,
-                                     uint2* __restrict__ stk, bool any_rt = false) {
+                                     uint2* __restrict__ stk, bool any_rt = false,
+                                     float4* __restrict__ lbuf = nullptr) {
     const bool kAnyHit = kDynAny ? any_rt : kAnyHitT;
     const uint32_t D = S.max_depth;
     const uint32_t G = 1u << D;
@@ -210,6 +211,54 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
     // wave-uniform (scalar) loads and broadcast; otherwise each lane loads its
     // own, kChunk loads in flight.
     auto leaf = [&](uint32_t off, uint32_t cnt) -> bool {
+        if (kLdsLeaf) {
+            // Wave-uniform leaf (the usual case: the lanes are one pixel's
+            // samples): the active lanes fetch the leaf's spheres once, one
+            // sphere per lane, into the wave's LDS buffer, and every lane then
+            // reads them by LDS broadcast.  A wave-wide dwordx4 load returns
+            // 1 KB through the texture-data path per sphere, which PMC shows
+            // ~96% busy; this returns 16 B per sphere.  Same spheres, same
+            // order, same tests as the vector path below.
+            const uint32_t uoff = __builtin_amdgcn_readfirstlane(off);
+            const uint32_t ucnt = __builtin_amdgcn_readfirstlane(cnt);
+            if (ucnt <= kLeafBuf && __all(off == uoff)) {
+                const uint64_t act = __ballot(1);
+                const uint32_t n_act = static_cast<uint32_t>(__popcll(act));
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                    static_cast<uint32_t>(act >> 32),
+                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(act), 0u));
+                for (uint32_t i = rank; i < ucnt; i += n_act) lbuf[i] = prim_sp[uoff + i];
+                // one wave's LDS operations complete in order: no barrier needed
+                for (uint32_t j = 0; j < ucnt; j += 2) {
+                    const float4 s0 = lbuf[j];
+                    const float4 s1 = lbuf[min(j + 1u, ucnt - 1u)];
+                    if (test(s0, uoff + j)) return true;
+                    if (j + 1u < ucnt && test(s1, uoff + j + 1u)) return true;
+                }
+                return false;
+            }
+        }
+        if (kSmemLeaf) {
+            // Wave-uniform leaf read by the SCALAR unit: 4 spheres (64 B) per
+            // scalar load straight into SGPRs, which the sphere tests take as
+            // operands.  Nothing is written into 64 lanes' VGPRs (a wave-wide
+            // dwordx4 load writes 1 KB of VGPRs per sphere).  Reads past the
+            // leaf end stay inside the arrays' 4-sphere padding.
+            const uint32_t uoff = __builtin_amdgcn_readfirstlane(off);
+            const uint32_t ucnt = __builtin_amdgcn_readfirstlane(cnt);
+            if (__all(off == uoff)) {
+                const float4* __restrict__ ps = prim_sp + uoff;
+                for (uint32_t j = 0; j < ucnt; j += 4) {
+                    float4 sv[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) sv[q] = ps[j + q];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (j + q < ucnt && test(sv[q], uoff + j + q)) return true;
+                }
+                return false;
+            }
+        }
         if (kUni) {
             const uint32_t uoff = __builtin_amdgcn_readfirstlane(off);
             if (__all(off == uoff)) {
@@ -629,12 +678,13 @@ __device__ __forceinline__ PixelOut sample_color(const FrameArgs& a, uint32_t x,
 
 // Unified lane path: one walk instance run twice (primary, then the shadow ray
 // of the lanes that need one), so the register allocator sees one walk.
-template <int kChunk, bool kStats>
+// kLeafMode: 0 vector loads, 1 LDS-staged uniform leaves, 2 scalar-loaded uniform leaves
+template <int kChunk, bool kStats, int kLeafMode = 0>
 __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uint32_t x,
                                                          uint32_t y, uint32_t hp, uint32_t s,
                                                          bool valid, uint32_t& n_shadow,
                                                          uint32_t& n_nodes, uint32_t& n_prims,
-                                                         void* stk) {
+                                                         void* stk, float4* lbuf = nullptr) {
     const SceneArgs& S = a.sc;
     float u = static_cast<float>(x), v = static_cast<float>(y);
     if (a.jitter) {
@@ -653,9 +703,9 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
         uint32_t idx = 0;
         bool hit = false;
         if (active)
-            hit = walk<false, kChunk, false, true, kStats>(S, r0, r1, r2, d0, d1, d2, 0.0f, INFINITY,
-                                                           t, idx, n_nodes, n_prims,
-                                                           static_cast<uint2*>(stk), any);
+            hit = walk<false, kChunk, false, true, kStats, kLeafMode == 1, kLeafMode == 2>(
+                S, r0, r1, r2, d0, d1, d2, 0.0f, INFINITY, t, idx, n_nodes, n_prims,
+                static_cast<uint2*>(stk), any, lbuf);
         if (phase == 0) {
             hit0 = active && hit;
             bool want_shadow = false;
@@ -701,8 +751,10 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
 // (ox, oy); for a packed tile list also (k, olx, oly) = slot and tile-local
 // origin.  Rounds of spw samples, pairwise butterfly per round, rounds added
 // in order in the leader's LDS slot, then the mean is written.
-template <bool kTiles, uint32_t kVar, int kChunk, bool kUni, bool kStats, bool kProg>
+template <bool kTiles, uint32_t kVar, int kChunk, bool kUni, bool kStats, bool kProg,
+          int kLeafMode>
 __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc, void* stk,
+                                                float4* lbuf,
                                                 uint32_t ox, uint32_t oy, uint32_t k,
                                                 uint32_t olx, uint32_t oly, uint32_t& n_primary,
                                                 uint32_t& n_shadow, uint32_t& n_nodes,
@@ -729,8 +781,8 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
         const bool valid = lane_ok && sg < s_end;
         n_primary += valid ? 1u : 0u;
         PixelOut c = kVar == kVariantLaneUnified
-                         ? sample_color_unified<kChunk, kStats>(a, x, y, hp, sg, valid, n_shadow,
-                                                                n_nodes, n_prims, stk)
+                         ? sample_color_unified<kChunk, kStats, kLeafMode>(
+                               a, x, y, hp, sg, valid, n_shadow, n_nodes, n_prims, stk, lbuf)
                          : sample_color<kVar, kChunk, kUni>(a, x, y, hp, sg, valid, n_shadow,
                                                             n_nodes, n_prims, stk);
         // Pixel sum of this round: pairwise butterfly over the pixel's g
@@ -787,7 +839,7 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
 // kProg: progressive frame (a.accum set); compiled separately so plain frames
 // keep their register budget.
 template <bool kTiles, uint32_t kVar, int kMinW, int kChunk, bool kUni, bool kStats = true,
-          bool kProg = false, bool kWaveQ = false>
+          bool kProg = false, bool kWaveQ = false, int kLeafMode = 0>
 __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     float4* acc = lds;  // [256] running pixel sums (leader lanes' slots)
@@ -797,6 +849,12 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
         stk = reinterpret_cast<PStackEntry*>(lds + kBlockThreads) + wave * a.stack_entries;
     else
         stk = reinterpret_cast<uint2*>(lds + kBlockThreads) + threadIdx.x;
+    // per-wave leaf buffer after the ancestor stacks (scene_lds_bytes)
+    float4* lbuf = nullptr;
+    if (kLeafMode == 1) {
+        const uint32_t levels = a.sc.max_depth > 1 ? a.sc.max_depth - 1 : 1;
+        lbuf = lds + kBlockThreads + levels * (kBlockThreads / 2) + wave * kLeafBuf;
+    }
     const uint32_t tw = a.tw, th = a.th;
     uint32_t n_shadow = 0, n_nodes = 0, n_prims = 0, n_primary = 0;
     if (kWaveQ) {
@@ -839,8 +897,8 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
                     ox += (tile % a.tiles_x) * a.tile_size;
                     oy += (tile / a.tiles_x) * a.tile_size;
                 }
-                shade_wave_tile<kTiles, kVar, kChunk, kUni, kStats, kProg>(
-                    a, acc, stk, ox, oy, k, olx, oly, n_primary, n_shadow, n_nodes, n_prims);
+                shade_wave_tile<kTiles, kVar, kChunk, kUni, kStats, kProg, kLeafMode>(
+                    a, acc, stk, lbuf, ox, oy, k, olx, oly, n_primary, n_shadow, n_nodes, n_prims);
             }
         }
     } else {
@@ -873,9 +931,9 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
             }
             for (uint32_t wt = wave; wt < wtiles; wt += kBlockThreads / 64) {
                 const uint32_t wox = (wt % wtx) * tw, woy = (wt / wtx) * th;
-                shade_wave_tile<kTiles, kVar, kChunk, kUni, kStats, kProg>(
-                    a, acc, stk, ox + wox, oy + woy, k, olx + wox, oly + woy, n_primary, n_shadow,
-                    n_nodes, n_prims);
+                shade_wave_tile<kTiles, kVar, kChunk, kUni, kStats, kProg, kLeafMode>(
+                    a, acc, stk, lbuf, ox + wox, oy + woy, k, olx + wox, oly + woy, n_primary,
+                    n_shadow, n_nodes, n_prims);
             }
         }
     }
@@ -922,7 +980,10 @@ size_t scene_lds_bytes(const FrameArgs& a) {
     if (a.variant == kVariantPacket)
         return colours + static_cast<size_t>(a.stack_entries) * (kBlockThreads / 64) * sizeof(PStackEntry);
     const uint32_t levels = a.sc.max_depth > 1 ? a.sc.max_depth - 1 : 1;
-    return colours + static_cast<size_t>(levels) * kBlockThreads * sizeof(uint2);
+    const size_t leafbuf = a.variant == kVariantWaveQLds
+                               ? static_cast<size_t>(kBlockThreads / 64) * kLeafBuf * sizeof(float4)
+                               : 0;
+    return colours + static_cast<size_t>(levels) * kBlockThreads * sizeof(uint2) + leafbuf;
 }
 
 // Resident workgroups on the device for a kernel at a given LDS size.  The
@@ -1043,6 +1104,26 @@ static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStr
         case kVariantLaneUnified1Stats:  // A/B only: variant 8 with the work counters compiled in
             launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 1, false, true>, a, n_bt,
                               lds, st);
+            break;
+        case kVariantWaveQLds:  // 13 + wave-uniform leaves staged through LDS
+            if (a.count_work)
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true, false, true,
+                                          1>,
+                             a, lds, st);
+            else
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, false, true,
+                                          1>,
+                             a, lds, st);
+            break;
+        case kVariantWaveQSmem:  // 13 + wave-uniform leaves read by scalar loads
+            if (a.count_work)
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true, false, true,
+                                          2>,
+                             a, lds, st);
+            else
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, false, true,
+                                          2>,
+                             a, lds, st);
             break;
         case kVariantWaveQ:  // per-wave scheduling over per-XCD queues
             if (a.count_work)

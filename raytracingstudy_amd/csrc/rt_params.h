@@ -25,6 +25,10 @@ constexpr uint32_t kVariantLaneUnified1Stats = 9;    // A/B: 8 with counters alw
 constexpr uint32_t kVariantLaneUnified2NoStats = 10; // A/B: 7 with counters only in stats frames
 constexpr uint32_t kVariantWaveQ = 13;     // unified walk scheduled per wave over per-XCD queues
                                            // (default for spp >= 8)
+constexpr uint32_t kVariantWaveQLds = 14;  // 13 + wave-uniform leaves fetched once into LDS
+constexpr uint32_t kLeafBuf = 16;          // spheres per wave in the LDS leaf buffer
+constexpr uint32_t kVariantWaveQSmem = 15; // 13 + wave-uniform leaves read by scalar loads
+constexpr uint32_t kPrimPad = 4;           // prim_sp padding: scalar reads may run 3 past a leaf
 
 // A/B toggles (rt_config.flags bits 20..23), results identical either way
 constexpr uint32_t kOptBtsShift = 1;       // bits 1..3: force the block-tile side (A/B):
