@@ -142,7 +142,8 @@ __device__ __forceinline__ bool isect(float o0, float o1, float o2, float d0, fl
 // kAnyHit: compile-time any-hit; with kDynAny the mode comes from `any_rt`
 // instead, so ONE inlined walk serves both the primary and the shadow ray.
 template <bool kAnyHitT, int kChunk = 4, bool kUni = false, bool kDynAny = false,
-          bool kStats = true, bool kLdsLeaf = false, bool kSmemLeaf = false>
+          bool kStats = true, bool kLdsLeaf = false, bool kSmemLeaf = false,
+          bool kLaneLeaf = false>
 __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, float o2, float d0,
                                      float d1, float d2, float tmin, float tmax, float& tout,
                                      uint32_t& iout, uint32_t& n_nodes, uint32_t& n_prims,
@@ -234,6 +235,38 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                     const float4 s1 = lbuf[min(j + 1u, ucnt - 1u)];
                     if (test(s0, uoff + j)) return true;
                     if (j + 1u < ucnt && test(s1, uoff + j + 1u)) return true;
+                }
+                return false;
+            }
+        }
+        if (kLaneLeaf) {
+            // Wave-uniform leaf: only the first active lane loads each sphere
+            // (a one-lane vector load: L1-cached like the wave-wide one, a
+            // fraction of its address/data-path cycles) and readfirstlane
+            // broadcasts it into SGPRs for every lane's test.
+            const uint32_t uoff = __builtin_amdgcn_readfirstlane(off);
+            const uint32_t ucnt = __builtin_amdgcn_readfirstlane(cnt);
+            if (__all(off == uoff)) {
+                const uint32_t lane_id = __lane_id();
+                const uint32_t first = __builtin_amdgcn_readfirstlane(lane_id);
+                const float4* __restrict__ ps = prim_sp + uoff;
+                for (uint32_t j = 0; j < ucnt; j += 2) {
+                    float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+                    if (lane_id == first) {
+                        a0 = ps[j];
+                        a1 = ps[min(j + 1u, ucnt - 1u)];
+                    }
+                    float4 b0, b1;
+                    b0.x = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a0.x)));
+                    b0.y = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a0.y)));
+                    b0.z = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a0.z)));
+                    b0.w = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a0.w)));
+                    b1.x = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a1.x)));
+                    b1.y = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a1.y)));
+                    b1.z = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a1.z)));
+                    b1.w = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a1.w)));
+                    if (test(b0, uoff + j)) return true;
+                    if (j + 1u < ucnt && test(b1, uoff + j + 1u)) return true;
                 }
                 return false;
             }
@@ -678,7 +711,8 @@ __device__ __forceinline__ PixelOut sample_color(const FrameArgs& a, uint32_t x,
 
 // Unified lane path: one walk instance run twice (primary, then the shadow ray
 // of the lanes that need one), so the register allocator sees one walk.
-// kLeafMode: 0 vector loads, 1 LDS-staged uniform leaves, 2 scalar-loaded uniform leaves
+// kLeafMode: 0 vector loads, 1 LDS-staged uniform leaves, 2 scalar-loaded uniform
+// leaves, 3 one-lane loads + readfirstlane broadcast for uniform leaves
 template <int kChunk, bool kStats, int kLeafMode = 0>
 __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uint32_t x,
                                                          uint32_t y, uint32_t hp, uint32_t s,
@@ -703,7 +737,8 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
         uint32_t idx = 0;
         bool hit = false;
         if (active)
-            hit = walk<false, kChunk, false, true, kStats, kLeafMode == 1, kLeafMode == 2>(
+            hit = walk<false, kChunk, false, true, kStats, kLeafMode == 1, kLeafMode == 2,
+                       kLeafMode == 3>(
                 S, r0, r1, r2, d0, d1, d2, 0.0f, INFINITY, t, idx, n_nodes, n_prims,
                 static_cast<uint2*>(stk), any, lbuf);
         if (phase == 0) {
@@ -1113,6 +1148,16 @@ static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStr
             else
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, false, true,
                                           1>,
+                             a, lds, st);
+            break;
+        case kVariantWaveQLane:  // 13 + one-lane loads broadcast by readfirstlane
+            if (a.count_work)
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true, false, true,
+                                          3>,
+                             a, lds, st);
+            else
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, false, true,
+                                          3>,
                              a, lds, st);
             break;
         case kVariantWaveQSmem:  // 13 + wave-uniform leaves read by scalar loads

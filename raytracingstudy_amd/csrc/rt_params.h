@@ -28,6 +28,7 @@ constexpr uint32_t kVariantWaveQ = 13;     // unified walk scheduled per wave ov
 constexpr uint32_t kVariantWaveQLds = 14;  // 13 + wave-uniform leaves fetched once into LDS
 constexpr uint32_t kLeafBuf = 16;          // spheres per wave in the LDS leaf buffer
 constexpr uint32_t kVariantWaveQSmem = 15; // 13 + wave-uniform leaves read by scalar loads
+constexpr uint32_t kVariantWaveQLane = 16; // 13 + one-lane leaf loads, readfirstlane broadcast
 constexpr uint32_t kPrimPad = 4;           // prim_sp padding: scalar reads may run 3 past a leaf
 
 // A/B toggles (rt_config.flags bits 20..23), results identical either way
