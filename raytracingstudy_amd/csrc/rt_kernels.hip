@@ -897,13 +897,14 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
         const uint32_t gw = kTiles ? a.tile_size / tw : (a.W + tw - 1) / tw;
         const uint32_t gh = kTiles ? a.tile_size / th : (a.H + th - 1) / th;
         const uint32_t nbx = (gw + 7u) / 8u, nby = (gh + 7u) / 8u;
-        const uint32_t per_grid = nbx * nby * 64u;  // units incl. padding of edge blocks
-        const uint32_t n_units = kTiles ? a.n_tiles * per_grid : per_grid;
+        const uint32_t per_grid = nbx * nby;  // 8x8-wave-tile blocks per grid
+        const uint32_t n_blocks = kTiles ? a.n_tiles * per_grid : per_grid;
         const uint32_t grp = blockIdx.x & 7u;
         for (uint32_t hop = 0; hop < 8u; ++hop) {
             const uint32_t q = (grp + hop) & 7u;
-            const uint32_t lo = static_cast<uint32_t>((uint64_t)n_units * q / 8u);
-            const uint32_t hi = static_cast<uint32_t>((uint64_t)n_units * (q + 1u) / 8u);
+            // range q = whole blocks [n_blocks*q/8, n_blocks*(q+1)/8), 64 units each
+            const uint32_t lo = 64u * static_cast<uint32_t>((uint64_t)n_blocks * q / 8u);
+            const uint32_t hi = 64u * static_cast<uint32_t>((uint64_t)n_blocks * (q + 1u) / 8u);
             unsigned long long* head = a.counters + kWaveQueueBase + q * kWaveQueueStride;
             const uint32_t chunk = a.wq_chunk;  // wave tiles per ticket
             uint32_t u = hi, u_end = hi;
@@ -916,12 +917,12 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
                     u_end = min(u + chunk, hi);
                 }
                 const uint32_t cur = u++;
-                uint32_t k = 0, rem = cur;
+                const uint32_t bidx = cur >> 6, w = cur & 63u;
+                uint32_t k = 0, blk = bidx;
                 if (kTiles) {
-                    k = cur / per_grid;
-                    rem = cur - k * per_grid;
+                    k = bidx / per_grid;
+                    blk = bidx - k * per_grid;
                 }
-                const uint32_t blk = rem >> 6, w = rem & 63u;
                 const uint32_t wx = (blk % nbx) * 8u + (w & 7u);
                 const uint32_t wy = (blk / nbx) * 8u + (w >> 3);
                 if (wx >= gw || wy >= gh) continue;  // padding of an edge block
@@ -1090,6 +1091,7 @@ static void launch_waveq(K kernel, const FrameArgs& a, size_t lds, hipStream_t s
         units = (uint64_t)a.n_tiles * (a.tile_size / a.tw) * (a.tile_size / a.th);
     else
         units = (uint64_t)((a.W + a.tw - 1) / a.tw) * ((a.H + a.th - 1) / a.th);
+    // (the grid only sizes the launch; padding units of edge blocks are skipped)
     const uint64_t want = (units + kBlockThreads / 64 - 1) / (kBlockThreads / 64);
     const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(res, want)));
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlockThreads), lds, st, a);
@@ -1196,15 +1198,7 @@ hipError_t launch_scene(const FrameArgs& a_in, hipStream_t st) {
     FrameArgs a = a_in;
     if (a.accum) a.variant = kVariantLaneUnified;  // what launch_scene_t runs (LDS sizing)
     // wave mapping: spw samples x ppw pixels per wave (see scene_kernel)
-    a.spw = a.spp >= 64u ? 64u : a.spp;
-    a.g = 1;
-    while (a.g < a.spw) a.g *= 2u;  // lanes per pixel (butterfly width)
-    const uint32_t ppw = 64u / a.g;
-    a.ppw = ppw;
-    uint32_t lg = 0;
-    while ((1u << lg) < ppw) ++lg;
-    a.tw = 1u << ((lg + 1) / 2);
-    a.th = 1u << (lg / 2);
+    wave_tile_shape(a.spp, a.spw, a.g, a.ppw, a.tw, a.th);
     a.rounds = (a.spp + a.spw - 1) / a.spw;
     a.stack_entries = 8u * a.sc.max_depth + 8u;
     const size_t lds = scene_lds_bytes(a);

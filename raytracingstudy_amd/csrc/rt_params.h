@@ -43,6 +43,20 @@ constexpr uint32_t kWaveQueueBase = 16;
 constexpr uint32_t kWaveQueueStride = 16;
 constexpr uint32_t kCounterWords = kWaveQueueBase + 8 * kWaveQueueStride;
 
+// Wave mapping of the scene kernel: spw = min(spp, 64) samples of a pixel on
+// g = pow2ceil(spw) lanes, ppw = 64 / g pixels per wave as a tw x th tile.
+inline void wave_tile_shape(uint32_t spp, uint32_t& spw, uint32_t& g, uint32_t& ppw,
+                            uint32_t& tw, uint32_t& th) {
+    spw = spp >= 64u ? 64u : (spp ? spp : 1u);
+    g = 1;
+    while (g < spw) g *= 2u;
+    ppw = 64u / g;
+    uint32_t lg = 0;
+    while ((1u << lg) < ppw) ++lg;
+    tw = 1u << ((lg + 1) / 2);
+    th = 1u << (lg / 2);
+}
+
 // Pinhole camera (include/camera.h:9-56): K and R column-major like glm.
 struct CamArgs {
     float K[9];  // K[c*3+r]

@@ -17,15 +17,42 @@ def tile_grid(width: int, height: int, ts: int = 64):
     return (width + ts - 1) // ts, (height + ts - 1) // ts
 
 
-def tiles_for_rank(width: int, height: int, rank: int, world: int, ts: int = 64) -> np.ndarray:
+PLANS = ("interleave", "latin")
+
+
+def tiles_for_rank(width: int, height: int, rank: int, world: int, ts: int = 64,
+                   plan: str = "interleave") -> np.ndarray:
+    """Tile ids of one rank.
+
+    interleave: tile t -> rank t % R (row-major ids).
+    latin: the tile grid is cut into an R x R grid of compact regions and rank r
+      takes region (i, (i + r) mod R) of every region row i, so it gets one
+      region per region row and per region column.  The load is as
+      interleaved as above, but a rank's share is R compact pieces (L2
+      locality), listed region by region.
+    """
     tx, ty = tile_grid(width, height, ts)
-    return np.arange(rank, tx * ty, world, dtype=np.uint32)
+    if plan == "interleave":
+        return np.arange(rank, tx * ty, world, dtype=np.uint32)
+    if plan != "latin":
+        raise ValueError(f"unknown tile plan {plan!r}")
+    out = []
+    for i in range(world):
+        j = (i + rank) % world
+        r0, r1 = ty * i // world, ty * (i + 1) // world
+        c0, c1 = tx * j // world, tx * (j + 1) // world
+        for row in range(r0, r1):
+            out.extend(range(row * tx + c0, row * tx + c1))
+    return np.asarray(out, dtype=np.uint32)
 
 
-def slab_tiles(width: int, height: int, world: int, ts: int = 64) -> int:
+def slab_tiles(width: int, height: int, world: int, ts: int = 64,
+               plan: str = "interleave") -> int:
     """Tile slots per rank in the equal-size gather (max over ranks)."""
     tx, ty = tile_grid(width, height, ts)
-    return (tx * ty + world - 1) // world
+    if plan == "interleave":
+        return (tx * ty + world - 1) // world
+    return max(len(tiles_for_rank(width, height, k, world, ts, plan)) for k in range(world))
 
 
 def pack_reference(img: np.ndarray, tile_ids, ts: int = 64) -> np.ndarray:

@@ -108,3 +108,13 @@ def test_gloo_world2_gather_reproduces_frame(oracle):
     ref, _, _ = oracle.Scene(sp, al).render(w, h, scene_pose(), oracle.resize_intrinsic(w, h),
                                             spp=spp, radiance=False)
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("w,h,world", [(1920, 1080, 2), (1920, 1080, 4), (1920, 1080, 8),
+                                       (3840, 2160, 8), (100, 70, 3)])
+def test_latin_plan_partitions_the_frame(w, h, world):
+    # every tile exactly once; each rank gets one region per region row/column
+    ids = [T.tiles_for_rank(w, h, k, world, 64, "latin") for k in range(world)]
+    tx, ty = T.tile_grid(w, h)
+    assert np.array_equal(np.sort(np.concatenate(ids)), np.arange(tx * ty))
+    assert T.slab_tiles(w, h, world, 64, "latin") == max(len(x) for x in ids)

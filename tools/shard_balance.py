@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--tile-size", type=int, default=rt.configs.TILE_SIZE)
     ap.add_argument("--opt", type=int, default=0, help="rt_config opt-off/A-B bits")
     ap.add_argument("--variant", type=int, default=0, help="scene-kernel variant (0 default)")
+    ap.add_argument("--plan", default="interleave", choices=T.PLANS, help="tile plan")
     args = ap.parse_args()
     import torch
     cfg = rt.CONFIGS[args.config]
@@ -59,15 +60,15 @@ def main():
     r.render(None, stream.cuda_stream)
     full = timed(lambda: r.render(None, stream.cuda_stream))
     out = {"config": args.config, "full_ms": round(full, 3), "tile_size": args.tile_size,
-           "opt": args.opt, "variant": args.variant}
+           "opt": args.opt, "variant": args.variant, "plan": args.plan}
     ts = args.tile_size
     for n in [int(x) for x in args.ranks.split(",")]:
-        slab = torch.zeros(T.slab_tiles(cfg.width, cfg.height, n, ts) * ts * ts * 4,
+        slab = torch.zeros(T.slab_tiles(cfg.width, cfg.height, n, ts, args.plan) * ts * ts * 4,
                            dtype=torch.uint8, device="cuda")
         torch.cuda.synchronize()
         per = []
         for k in range(n):
-            ids = T.tiles_for_rank(cfg.width, cfg.height, k, n, ts)
+            ids = T.tiles_for_rank(cfg.width, cfg.height, k, n, ts, args.plan)
             r.render_tiles(ids, ts, slab.data_ptr(), stream.cuda_stream)
             per.append(timed(lambda: r.render_tiles(ids, ts, slab.data_ptr(), stream.cuda_stream)))
         # the same pixel count as one contiguous band of tile rows (locality check)
