@@ -141,9 +141,8 @@ __device__ __forceinline__ bool isect(float o0, float o1, float o2, float d0, fl
 // The per-thread ancestor stack lives in LDS, [depth-1][thread] (conflict-free).
 // kAnyHit: compile-time any-hit; with kDynAny the mode comes from `any_rt`
 // instead, so ONE inlined walk serves both the primary and the shadow ray.
-template <bool kAnyHitT, int kChunk = 4, bool kUni = false, bool kDynAny = false,
-          bool kStats = true, bool kLdsLeaf = false, bool kSmemLeaf = false,
-          bool kLaneLeaf = false>
+template <bool kAnyHitT, int kChunk = 4, bool kDynAny = false, bool kStats = true,
+          bool kLdsLeaf = false, bool kSmemLeaf = false, bool kLaneLeaf = false>
 __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, float o2, float d0,
                                      float d1, float d2, float tmin, float tmax, float& tout,
                                      uint32_t& iout, uint32_t& n_nodes, uint32_t& n_prims,
@@ -207,10 +206,9 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         return false;
     };
     // Leaf spheres in list order (same order, hence same counters, as the
-    // oracle).  kUni: when every active lane sits in the same leaf (the usual
-    // case: a wave traces the samples of one pixel) the spheres are read with
-    // wave-uniform (scalar) loads and broadcast; otherwise each lane loads its
-    // own, kChunk loads in flight.
+    // oracle): each lane loads its own, kChunk loads in flight.  kLdsLeaf /
+    // kSmemLeaf / kLaneLeaf are measured alternatives for wave-uniform leaves
+    // (variants 14-16), none faster.
     auto leaf = [&](uint32_t off, uint32_t cnt) -> bool {
         if (kLdsLeaf) {
             // Wave-uniform leaf (the usual case: the lanes are one pixel's
@@ -292,22 +290,6 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 return false;
             }
         }
-        if (kUni) {
-            const uint32_t uoff = __builtin_amdgcn_readfirstlane(off);
-            if (__all(off == uoff)) {
-                const uint32_t ucnt = __builtin_amdgcn_readfirstlane(cnt);
-                bool alive = true, hit = false;
-                for (uint32_t j = 0; j < ucnt; ++j) {
-                    const float4 sp = prim_sp[uoff + j];
-                    if (alive && test(sp, uoff + j)) {
-                        alive = false;
-                        hit = true;
-                    }
-                    if (kAnyHit && !__any(alive)) break;
-                }
-                return hit;
-            }
-        }
         const float4* __restrict__ ps = prim_sp + off;
         const uint32_t last = cnt - 1;
         for (uint32_t j = 0; j < cnt; j += kChunk) {
@@ -349,13 +331,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             const uint32_t valid = node.y & 0xFFu;
             if (valid & (1u << child)) {
                 const uint32_t slot = node.x + __builtin_popcount(valid & ((1u << child) - 1u));
-                uint2 rec;
-                if (kUni) {
-                    const uint32_t uslot = __builtin_amdgcn_readfirstlane(slot);
-                    rec = __all(slot == uslot) ? nodes[uslot] : nodes[slot];
-                } else {
-                    rec = nodes[slot];
-                }
+                const uint2 rec = nodes[slot];
                 if (kStats) n_nodes += 1;
                 if (!((node.y >> 8) & (1u << child))) {
                     node = rec;
@@ -642,7 +618,7 @@ __device__ __forceinline__ void flush_counters(const FrameArgs& a, uint32_t prim
 // One sample of pixel (x, y): primary walk, Lambert shade, shadow walk.
 // kVar selects the traversal; `valid` lanes trace, the others only take part
 // in the packet walks' wave-wide votes.
-template <uint32_t kVar, int kChunk, bool kUni>
+template <uint32_t kVar, int kChunk>
 __device__ __forceinline__ PixelOut sample_color(const FrameArgs& a, uint32_t x, uint32_t y,
                                                  uint32_t hp, uint32_t s, bool valid,
                                                  uint32_t& n_shadow, uint32_t& n_nodes,
@@ -662,7 +638,7 @@ __device__ __forceinline__ PixelOut sample_color(const FrameArgs& a, uint32_t x,
         hit = walk_packet<false>(S, valid, a.cam.o[0], a.cam.o[1], a.cam.o[2], d0, d1, d2, 0.0f, t,
                                  idx, n_nodes, n_prims, static_cast<PStackEntry*>(stk));
     } else if (valid) {
-        hit = walk<false, kChunk, kUni>(S, a.cam.o[0], a.cam.o[1], a.cam.o[2], d0, d1, d2, 0.0f, INFINITY,
+        hit = walk<false, kChunk>(S, a.cam.o[0], a.cam.o[1], a.cam.o[2], d0, d1, d2, 0.0f, INFINITY,
                                   t, idx, n_nodes, n_prims, static_cast<uint2*>(stk));
     }
     const float miss_r = 200.0f / 255.0f;
@@ -696,7 +672,7 @@ __device__ __forceinline__ PixelOut sample_color(const FrameArgs& a, uint32_t x,
         }
     } else if (want_shadow) {
         n_shadow += 1;
-        if (walk<true, kChunk, kUni>(S, s0, s1, s2, a.L[0], a.L[1], a.L[2], 0.0f, INFINITY, ts, is,
+        if (walk<true, kChunk>(S, s0, s1, s2, a.L[0], a.L[1], a.L[2], 0.0f, INFINITY, ts, is,
                                n_nodes, n_prims, static_cast<uint2*>(stk)))
             lam = 0.0f;
     }
@@ -737,7 +713,7 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
         uint32_t idx = 0;
         bool hit = false;
         if (active)
-            hit = walk<false, kChunk, false, true, kStats, kLeafMode == 1, kLeafMode == 2,
+            hit = walk<false, kChunk, true, kStats, kLeafMode == 1, kLeafMode == 2,
                        kLeafMode == 3>(
                 S, r0, r1, r2, d0, d1, d2, 0.0f, INFINITY, t, idx, n_nodes, n_prims,
                 static_cast<uint2*>(stk), any, lbuf);
@@ -786,8 +762,7 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
 // (ox, oy); for a packed tile list also (k, olx, oly) = slot and tile-local
 // origin.  Rounds of spw samples, pairwise butterfly per round, rounds added
 // in order in the leader's LDS slot, then the mean is written.
-template <bool kTiles, uint32_t kVar, int kChunk, bool kUni, bool kStats, bool kProg,
-          int kLeafMode>
+template <bool kTiles, uint32_t kVar, int kChunk, bool kStats, bool kProg, int kLeafMode>
 __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc, void* stk,
                                                 float4* lbuf,
                                                 uint32_t ox, uint32_t oy, uint32_t k,
@@ -818,7 +793,7 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
         PixelOut c = kVar == kVariantLaneUnified
                          ? sample_color_unified<kChunk, kStats, kLeafMode>(
                                a, x, y, hp, sg, valid, n_shadow, n_nodes, n_prims, stk, lbuf)
-                         : sample_color<kVar, kChunk, kUni>(a, x, y, hp, sg, valid, n_shadow,
+                         : sample_color<kVar, kChunk>(a, x, y, hp, sg, valid, n_shadow,
                                                             n_nodes, n_prims, stk);
         // Pixel sum of this round: pairwise butterfly over the pixel's g
         // lanes (missing samples are 0) = oracle.c:tree_sum; rounds are then
@@ -873,7 +848,7 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
 // kMinW = minimum waves per SIMD requested from the register allocator.
 // kProg: progressive frame (a.accum set); compiled separately so plain frames
 // keep their register budget.
-template <bool kTiles, uint32_t kVar, int kMinW, int kChunk, bool kUni, bool kStats = true,
+template <bool kTiles, uint32_t kVar, int kMinW, int kChunk, bool kStats = true,
           bool kProg = false, bool kWaveQ = false, int kLeafMode = 0>
 __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
@@ -933,7 +908,7 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
                     ox += (tile % a.tiles_x) * a.tile_size;
                     oy += (tile / a.tiles_x) * a.tile_size;
                 }
-                shade_wave_tile<kTiles, kVar, kChunk, kUni, kStats, kProg, kLeafMode>(
+                shade_wave_tile<kTiles, kVar, kChunk, kStats, kProg, kLeafMode>(
                     a, acc, stk, lbuf, ox, oy, k, olx, oly, n_primary, n_shadow, n_nodes, n_prims);
             }
         }
@@ -967,7 +942,7 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
             }
             for (uint32_t wt = wave; wt < wtiles; wt += kBlockThreads / 64) {
                 const uint32_t wox = (wt % wtx) * tw, woy = (wt / wtx) * th;
-                shade_wave_tile<kTiles, kVar, kChunk, kUni, kStats, kProg, kLeafMode>(
+                shade_wave_tile<kTiles, kVar, kChunk, kStats, kProg, kLeafMode>(
                     a, acc, stk, lbuf, ox + wox, oy + woy, k, olx + wox, oly + woy, n_primary,
                     n_shadow, n_nodes, n_prims);
             }
@@ -1102,94 +1077,78 @@ static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStr
     if (a.accum) {  // progressive frames: the unified walk, whatever the A/B variant
         if (a.spp >= 8u) {
             if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true, true, true>,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, true, true>,
                              a, lds, st);
             else
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true, true>,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true, true>,
                              a, lds, st);
         } else if (a.count_work) {
-            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true, true>, a,
+            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, true>, a,
                               n_bt, lds, st);
         } else {
-            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true>, a,
+            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true>, a,
                               n_bt, lds, st);
         }
         return;
     }
-    if (a.variant == kVariantLaneUnified1) {  // default: counters only in stats frames
-        if (a.count_work)
-            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 1, false, true>, a, n_bt,
-                              lds, st);
-        else
-            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 1, false, false>, a, n_bt,
-                              lds, st);
-        return;
-    }
     switch (a.variant) {
         case kVariantPacket:
-            launch_persistent(scene_kernel<kTiles, kVariantPacket, 1, 4, false>, a, n_bt, lds, st);
+            launch_persistent(scene_kernel<kTiles, kVariantPacket, 1, 4>, a, n_bt, lds, st);
             break;
         case kVariantLaneChunk2:
-            launch_persistent(scene_kernel<kTiles, kVariantLane, 1, 2, false>, a, n_bt, lds, st);
-            break;
-        case kVariantLaneUni1:
-            launch_persistent(scene_kernel<kTiles, kVariantLane, 1, 1, true>, a, n_bt, lds, st);
+            launch_persistent(scene_kernel<kTiles, kVariantLane, 1, 2>, a, n_bt, lds, st);
             break;
         case kVariantLaneUnified:
-            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false>, a, n_bt, lds, st);
-            break;
-        case kVariantLaneUnified1Stats:  // A/B only: variant 8 with the work counters compiled in
-            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 1, false, true>, a, n_bt,
-                              lds, st);
+            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2>, a, n_bt, lds, st);
             break;
         case kVariantWaveQLds:  // 13 + wave-uniform leaves staged through LDS
             if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true, false, true,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true,
                                           1>,
                              a, lds, st);
             else
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, false, true,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true,
                                           1>,
                              a, lds, st);
             break;
         case kVariantWaveQLane:  // 13 + one-lane loads broadcast by readfirstlane
             if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true, false, true,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true,
                                           3>,
                              a, lds, st);
             else
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, false, true,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true,
                                           3>,
                              a, lds, st);
             break;
         case kVariantWaveQSmem:  // 13 + wave-uniform leaves read by scalar loads
             if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true, false, true,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true,
                                           2>,
                              a, lds, st);
             else
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, false, true,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true,
                                           2>,
                              a, lds, st);
             break;
         case kVariantWaveQ:  // per-wave scheduling over per-XCD queues
             if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true, false, true>,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true>,
                              a, lds, st);
             else
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, false, true>,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true>,
                              a, lds, st);
             break;
         case kVariantLaneUnified2NoStats:  // A/B only: variant 7 without the work counters
             if (a.count_work)
-                launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true>, a, n_bt,
+                launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true>, a, n_bt,
                                   lds, st);
             else
-                launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false>, a,
+                launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false>, a,
                                   n_bt, lds, st);
             break;
         default:
-            launch_persistent(scene_kernel<kTiles, kVariantLane, 1, 4, false>, a, n_bt, lds, st);
+            launch_persistent(scene_kernel<kTiles, kVariantLane, 1, 4>, a, n_bt, lds, st);
             break;
     }
 }

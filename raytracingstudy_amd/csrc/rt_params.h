@@ -18,10 +18,7 @@ constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr uint32_t kVariantLane = 1;    // one ray per lane, per-thread LDS ancestor stack
 constexpr uint32_t kVariantPacket = 2;  // 64-ray wave packet, per-wave LDS stack, ballot masks
 constexpr uint32_t kVariantLaneChunk2 = 3;  // lane walk, 2 leaf spheres in flight (fewer VGPRs)
-constexpr uint32_t kVariantLaneUni1 = 4;    // lane walk + wave-uniform scalar leaf/node path, 1 in flight
 constexpr uint32_t kVariantLaneUnified = 7;   // one walk instance for primary + shadow, 2 in flight
-constexpr uint32_t kVariantLaneUnified1 = 8;  // same, 1 in flight; counters only in stats frames
-constexpr uint32_t kVariantLaneUnified1Stats = 9;    // A/B: 8 with counters always compiled in
 constexpr uint32_t kVariantLaneUnified2NoStats = 10; // A/B: 7 with counters only in stats frames
 constexpr uint32_t kVariantWaveQ = 13;     // unified walk scheduled per wave over per-XCD queues
                                            // (default for spp >= 8)
