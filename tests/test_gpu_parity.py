@@ -344,3 +344,24 @@ def test_graphics_resource_binding_plumbing(gpu):
         r.synchronize()
         assert np.array_equal(buf.cpu().numpy().reshape(48, 64, 4), ref)
     assert lib.rt_bind_graphics_resource(None, None) == rt._lib.RT_E_INVALID
+
+
+@pytest.mark.parametrize("spp", [65, 127])
+def test_scene_partial_last_round(gpu, oracle, spp):
+    """spp > 64 and not a multiple of it: the last round has 1 (or 63) samples
+    on a 64-lane butterfly (missing samples are 0 in the pairwise sum)."""
+    img, rad, st, info, ref8, ref32, cnt, _ = _scene_pair(oracle, 5000, 48, 32, spp)
+    assert np.array_equal(img, ref8)
+    assert np.array_equal(rad, ref32)
+    _check_counts(st, cnt, 0)
+
+
+def test_scene_8k_frame_rows(gpu, oracle):
+    """8192x4320 (35.4 M pixels, > 2^24): pixel ids, jitter hashes and the
+    output index at full width; every 540th row against the oracle."""
+    img, rad, st, info, ref8, ref32, cnt, _ = _scene_pair(oracle, 20000, 8192, 4320, 1,
+                                                           row_step=540)
+    rows = np.arange(0, 4320, 540)
+    assert np.array_equal(img[rows], ref8[rows])
+    assert np.array_equal(rad[rows], ref32[rows])
+    assert st.primary_rays == 8192 * 4320
