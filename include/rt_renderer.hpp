@@ -114,6 +114,20 @@ public:
         check(rt_save_spheres(path.c_str(), spheres.data(), albedo.empty() ? nullptr : albedo.data(),
                               static_cast<uint32_t>(spheres.size() / 4)));
     }
+    // multi-GPU: render only the listed 64x64 tiles into a packed device slab
+    // (rt_render_tiles), and scatter packed slabs into a frame (rt_unpack_tiles)
+    void renderTiles(const std::vector<uint32_t>& ids, uint32_t tile_size, void* dev_packed,
+                     void* stream = nullptr, rt_stats* stats = nullptr) {
+        check(rt_render_tiles(r_, ids.data(), static_cast<uint32_t>(ids.size()), tile_size,
+                              dev_packed, stream, stats),
+              r_);
+    }
+    void unpackTiles(const void* dev_packed, const std::vector<uint32_t>& ids, uint32_t tile_size,
+                     void* dev_rgba8 = nullptr, void* stream = nullptr) {
+        check(rt_unpack_tiles(r_, dev_packed, ids.data(), static_cast<uint32_t>(ids.size()),
+                              tile_size, dev_rgba8, stream),
+              r_);
+    }
     rt_scene_info sceneInfo() const {
         rt_scene_info i;
         check(rt_get_scene_info(r_, &i), r_);

@@ -56,3 +56,21 @@ def test_cli_scene_file_roundtrip_and_builders(gpu, tmp_path):
         assert "3000 spheres" in r.stdout
         outs.append(o.read_bytes())
     assert outs[0] == outs[1] == outs[2]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gpus", [2, 3])
+def test_cli_multi_renderer_frame_equals_single(gpu, tmp_path, gpus):
+    """rt_cli --gpus N (one process, N renderers, peer gather to device 0),
+    rehearsed with all renderers on device 0: the assembled frame equals the
+    single-renderer frame byte for byte."""
+    base = [CLI, "--config", "c3", "--spheres", "20000", "--width", "200", "--height", "150",
+            "--spp", "8", "--frames", "2"]
+    one, many = tmp_path / "one.ppm", tmp_path / "many.ppm"
+    r1 = subprocess.run(base + ["--out", str(one)], capture_output=True, text=True, timeout=120)
+    assert r1.returncode == 0, r1.stderr
+    rn = subprocess.run(base + ["--gpus", str(gpus), "--same-device", "--out", str(many)],
+                        capture_output=True, text=True, timeout=120)
+    assert rn.returncode == 0, rn.stderr
+    assert f"{gpus} renderers" in rn.stdout
+    assert one.read_bytes() == many.read_bytes()
