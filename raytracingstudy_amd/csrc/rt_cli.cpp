@@ -8,6 +8,12 @@
 //   rt_cli [--config c1|c2|c3|c4|c5] [--width W --height H --spp S --spheres N
 //           --depth D] [--frames F] [--out image.ppm] [--scene in.rtsph]
 //          [--save-scene out.rtsph] [--host-build] [--gpus N [--same-device]]
+//          [--progressive] [--panel] [--walk]
+//
+// --panel prints the stats panel (rt_camera.hpp StatsPanel: the reference's
+// ImGui window numbers plus Mrays/s, spp, GPUs) after every frame; --walk
+// moves the camera through the Displayer's controller (W held every frame);
+// --progressive accumulates samples while the camera stays put.
 //
 // --gpus N: one process drives N devices: renderer k renders
 // the 64x64 tiles t = k, k+N, ... into a packed slab on device k; the slabs
@@ -26,6 +32,7 @@
 
 #include <memory>
 
+#include "../../include/rt_camera.hpp"
 #include "../../include/rt_renderer.hpp"
 
 namespace {
@@ -149,7 +156,8 @@ int run_multi(rtamd::KernelRenderer& r0, const rt_config& rc, const float pose[1
 
 int main(int argc, char** argv) {
     std::string cfg = "c2", out, scene_in, scene_out;
-    bool host_build = false, same_device = false;
+    bool host_build = false, same_device = false, progressive = false, panel = false,
+         walk = false;
     int gpus = 1;
     int W = 0, H = 0, spp = 0, frames = 3;
     long n = -1;
@@ -175,6 +183,9 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--host-build")) host_build = true;
         else if (!strcmp(argv[i], "--gpus")) gpus = atoi(next("--gpus"));
         else if (!strcmp(argv[i], "--same-device")) same_device = true;
+        else if (!strcmp(argv[i], "--progressive")) progressive = true;
+        else if (!strcmp(argv[i], "--panel")) panel = true;
+        else if (!strcmp(argv[i], "--walk")) walk = true;
         else {
             fprintf(stderr, "unknown argument %s\n", argv[i]);
             return 2;
@@ -206,6 +217,7 @@ int main(int argc, char** argv) {
         rc.spp = spp;
         rc.mode = c->mode;
         if (host_build) rc.flags |= RT_FLAG_HOST_BUILD;
+        if (progressive) rc.flags |= RT_FLAG_PROGRESSIVE;
         rtamd::KernelRenderer r(rc);
         r.resize(W, H);
         // Displayer default orientation (include/window/displayer.h:47-52):
@@ -240,12 +252,27 @@ int main(int argc, char** argv) {
         }
         rt_stats st{};
         double best = 1e30;
+        // the Displayer's controller, starting at this config's camera position
+        rtamd::CameraController cam;
+        for (int i = 0; i < 3; ++i) cam.pos[i] = pose[12 + i];
+        rtamd::StatsPanel stats_panel;
         for (int f = 0; f < frames; ++f) {
-            r.setPosition(pose);  // every frame, like Displayer::processInput
             auto t0 = std::chrono::steady_clock::now();
+            if (walk) {
+                rtamd::Keys k;
+                k.w = true;
+                cam.processInput(k, r);  // like Displayer::processInput, every frame
+            } else {
+                r.setPosition(pose);
+            }
             r.render(nullptr, nullptr, &st);
             auto t1 = std::chrono::steady_clock::now();
-            best = std::min(best, std::chrono::duration<double, std::milli>(t1 - t0).count());
+            const double ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+            best = std::min(best, ms);
+            if (panel) {
+                stats_panel.update(ms, st, 1);
+                printf("-- frame %d --\n%s", f, stats_panel.text().c_str());
+            }
         }
         const double rays = (double)st.primary_rays + (double)st.shadow_rays;
         printf("%s %dx%d spp %d: kernel %.3f ms, wall %.3f ms, %.0f rays (%llu primary + %llu shadow), "

@@ -74,3 +74,20 @@ def test_cli_multi_renderer_frame_equals_single(gpu, tmp_path, gpus):
     assert rn.returncode == 0, rn.stderr
     assert f"{gpus} renderers" in rn.stdout
     assert one.read_bytes() == many.read_bytes()
+
+
+@pytest.mark.gpu
+def test_cli_panel_progressive_and_walk(gpu):
+    """The stats panel (rt_camera.hpp) through the native driver: progressive
+    frames accumulate spp while the camera stays put; walking restarts it."""
+    base = [CLI, "--config", "c3", "--spheres", "20000", "--width", "160", "--height", "120",
+            "--spp", "4", "--frames", "3", "--panel", "--progressive"]
+    r = subprocess.run(base, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    spp = [int(l.split()[1]) for l in r.stdout.splitlines() if l.startswith("spp ")]
+    assert spp == [4, 8, 12]
+    assert "Mrays/s" in r.stdout and "GPUs 1" in r.stdout and "frames 3" in r.stdout
+    r = subprocess.run(base + ["--walk"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    spp = [int(l.split()[1]) for l in r.stdout.splitlines() if l.startswith("spp ")]
+    assert spp == [4, 4, 4]  # every step moves the camera: accumulation restarts
