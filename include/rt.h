@@ -82,8 +82,9 @@ enum {
     RT_FLAG_PROGRESSIVE = 1u << 5, /* scene mode: accumulate samples across frames while the
                                       camera, size, scene and tile list stay unchanged; every
                                       frame adds spp samples */
-    /* bits 16..19: scene-kernel variant for A/B runs (0 = default = 1, one ray
-     * per lane; 2 = 64-ray wave packets); images are identical */
+    /* bits 16..19: scene-kernel variant for A/B runs (0 = default: 13, the
+     * per-wave queue, for spp >= 8, else 7; others in DESIGN.md 5.1); images
+     * and counters are identical across variants (packets: images only) */
     RT_FLAG_VARIANT_SHIFT = 16,
     /* bits 20..27: A/B toggles that switch single optimisations off or on (0 = defaults) */
     RT_FLAG_OPT_SHIFT = 20

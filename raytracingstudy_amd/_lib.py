@@ -35,8 +35,10 @@ RT_BUILDER_DEVICE = 0
 RT_BUILDER_HOST = 1
 RT_FLAG_VARIANT_SHIFT = 16
 RT_FLAG_OPT_SHIFT = 20
-VARIANT_LANE = 1    # one ray per lane
-VARIANT_PACKET = 2  # 64-ray wave packets (default)
+VARIANT_LANE = 1    # one ray per lane, separate primary/shadow walks (A/B)
+VARIANT_PACKET = 2  # 64-ray wave packets (A/B)
+VARIANT_BLOCK = 7   # unified walk, block-tile queue (default for spp < 8)
+VARIANT_WAVEQ = 13  # unified walk, per-wave per-XCD queues (default for spp >= 8)
 
 _f3 = ctypes.c_float * 3
 
