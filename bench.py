@@ -53,6 +53,9 @@ def parse():
                          "the multi-rank path on one GPU)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal: every rank uses cuda:0 (with --backend gloo)")
+    ap.add_argument("--secondary", default="c2,c5",
+                    help="N=1 only: also time these configs (a few frames each) and report them "
+                         "under `secondary`; '' to skip")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="PMC traffic summary written by tools/pmc_traffic.py")
     return ap.parse_args()
@@ -93,6 +96,40 @@ def cpu_baseline(cfg, K, pose, target_s: float) -> dict:
                       f"{cfg.spp} spp = {int(c[0])} primary + {int(c[1])} shadow rays) in {el:.1f} s",
             "single_core": {"value": round(rays1 / el1 / 1e6, 3), "unit": "Mrays/s", "cores": 1,
                             "sample": f"every {s1}th row ({rays1} rays) in {el1:.2f} s"}}
+
+
+def secondary_config(rt, torch, name: str, dev, stream, steps: int = 3) -> dict:
+    """Time another BASELINE config on this GPU: kernel ms (HIP events on the
+    launch stream), Mrays/s from the counted rays, scene build time."""
+    import numpy as np
+    from raytracingstudy_amd.camera import scene_pose
+
+    c = rt.CONFIGS[name]
+    sp, al = rt.generate_spheres(c.n_spheres, rt.SEED)
+    r2 = rt.KernelRenderer(c.width, c.height, mode="scene", spp=c.spp, device=dev.index)
+    try:
+        r2.resize(c.width, c.height)
+        r2.setPosition(scene_pose())
+        info = r2.set_scene(sp, al, max_depth=c.max_depth)
+        st = r2.render(None, stream.cuda_stream, stats=True)
+        rays = st.primary_rays + st.shadow_rays
+        ms = []
+        for _ in range(steps):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            r2.render(None, stream.cuda_stream)
+            e1.record(stream)
+            e1.synchronize()
+            ms.append(e0.elapsed_time(e1))
+        k = float(np.median(ms))
+        return {"workload": f"{c.width}x{c.height}, {c.spp} spp, {c.n_spheres} spheres, "
+                            f"depth {info['max_depth']}",
+                "kernel_ms": round(k, 3), "Mrays_s": round(rays / k / 1e3, 1),
+                "rays_per_frame": int(rays), "scene_build_ms": round(info["build_ms"], 2),
+                "octree_nodes": info["n_nodes"], "prim_refs": info["n_prim_refs"]}
+    finally:
+        r2.close()
 
 
 def main():
@@ -283,6 +320,13 @@ def main():
             r.render(whole.data_ptr(), sptr)
             torch.cuda.synchronize(dev)
             out["config"]["tiles_frame_check"] = bool(torch.equal(whole, frame))
+        if world == 1 and not args.shard and args.secondary:
+            out["secondary"] = {}
+            for name in [c for c in args.secondary.split(",") if c and c != cfg.name]:
+                try:
+                    out["secondary"][name] = secondary_config(rt, torch, name, dev, stream)
+                except Exception as e:  # reported, never fatal for the headline
+                    out["secondary"][name] = {"error": repr(e)}
         if world == 1 and args.cpu_baseline == "auto":
             try:
                 out["cpu_baseline"] = cpu_baseline(cfg, K, pose, args.cpu_seconds)
