@@ -6,7 +6,7 @@
 TAG=${1:-deep}; CFG=${2:-c3}; EXTRA=${3:-}; SET=${4:-sq}
 ROOT=$(pwd); OUT=$ROOT/gpurun_out/pmc_$TAG; mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="$ROOT/bench.py --steps 2 --warmup 0 --config $CFG --cpu-baseline off $EXTRA"
+BENCH="$ROOT/bench.py --steps 2 --warmup 0 --config $CFG --cpu-baseline off --secondary= $EXTRA"
 cd /tmp || exit 1
 i=0
 while read -r COUNTERS; do

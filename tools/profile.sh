@@ -14,7 +14,7 @@ ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="$ROOT/bench.py --steps $STEPS --warmup 1 --config $CFG --cpu-baseline off"
+BENCH="$ROOT/bench.py --steps $STEPS --warmup 1 --config $CFG --cpu-baseline off --secondary="
 cd /tmp || exit 1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/trace" -o run \
     -- python3 $BENCH > "$OUT/trace.log" 2>&1 &&
