@@ -87,7 +87,11 @@ enum {
      * and counters are identical across variants (packets: images only) */
     RT_FLAG_VARIANT_SHIFT = 16,
     /* bits 20..27: A/B toggles that switch single optimisations off or on (0 = defaults) */
-    RT_FLAG_OPT_SHIFT = 20
+    RT_FLAG_OPT_SHIFT = 20,
+    /* bits 28..31: depth of the octree's cell table (DESIGN.md 5.1 "Cell table"):
+     * 0 = chosen from the tree (default), 1..7 = that depth (clamped to the
+     * tree), 15 = no table.  Images and counters are the same either way. */
+    RT_FLAG_CELL_TABLE_SHIFT = 28
 };
 
 typedef struct rt_config {
@@ -137,7 +141,7 @@ typedef struct rt_scene_info {
                                 build + upload with RT_FLAG_HOST_BUILD)                 */
     double upload_ms;        /* time to place the sphere list in device memory          */
     uint32_t builder;        /* RT_BUILDER_* that built the current tree                */
-    uint32_t reserved;
+    uint32_t cell_table_depth; /* K of the depth-K cell table the walk uses, 0 = none   */
 } rt_scene_info;
 
 enum { RT_BUILDER_DEVICE = 0, RT_BUILDER_HOST = 1 };

@@ -35,6 +35,8 @@ RT_BUILDER_DEVICE = 0
 RT_BUILDER_HOST = 1
 RT_FLAG_VARIANT_SHIFT = 16
 RT_FLAG_OPT_SHIFT = 20
+RT_FLAG_CELL_TABLE_SHIFT = 28
+RT_CELL_TABLE_OFF = 15
 VARIANT_LANE = 1    # one ray per lane, separate primary/shadow walks (A/B)
 VARIANT_PACKET = 2  # 64-ray wave packets (A/B)
 VARIANT_BLOCK = 7   # unified walk, block-tile queue (default for spp < 8)
@@ -96,11 +98,11 @@ class RtSceneInfo(ctypes.Structure):
         ("build_ms", ctypes.c_double),
         ("upload_ms", ctypes.c_double),
         ("builder", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("cell_table_depth", ctypes.c_uint32),
     ]
 
     def as_dict(self) -> dict:
-        d = {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+        d = {f: getattr(self, f) for f, _ in self._fields_}
         d["builder"] = "host" if self.builder == RT_BUILDER_HOST else "device"
         d["root_min"] = list(self.root_min)
         d["root_max"] = list(self.root_max)

@@ -76,4 +76,30 @@ private:
     uint4* totals_host_ = nullptr;
 };
 
+// Depth-K cell table over a built octree (cell_table.hip): one uint2 entry per
+// depth-K cell naming the node that covers it, so a walk can reach depth K in
+// one load.  k_req: kCellTableAuto (choose K from the tree), kCellTableOff, or
+// a depth (clamped to the tree).  k() == 0 means no table (root leaf, or a
+// leaf list longer than the packed entry holds).
+class CellTable {
+public:
+    CellTable() = default;
+    CellTable(const CellTable&) = delete;
+    CellTable& operator=(const CellTable&) = delete;
+    ~CellTable() { release(); }
+    hipError_t build(const uint2* nodes, uint2 root, bool root_is_leaf, uint32_t max_depth,
+                     uint32_t depth_reached, uint32_t k_req, hipStream_t st);
+    void release();
+    const uint2* table() const { return k_ ? tab_ : nullptr; }
+    uint32_t k() const { return k_; }
+
+private:
+    hipError_t run(const uint2* nodes, uint2 root, uint32_t K, bool write, hipStream_t st,
+                   unsigned long long* hist_host, uint32_t* overflow_host);
+    uint2* tab_ = nullptr;
+    size_t cap_ = 0;
+    unsigned long long* scratch_ = nullptr;
+    uint32_t k_ = 0;
+};
+
 }  // namespace rtamd

@@ -79,6 +79,7 @@ struct rt_renderer {
     rt_octree_params oct;
     bool has_scene = false;
     GpuOctreeBuilder gpu_build;
+    CellTable cell_table;
     DevBuf<uint2> d_nodes;
     DevBuf<float4> d_prim_sp;
     DevBuf<uint32_t> d_prim_idx;
@@ -248,6 +249,17 @@ int build_scene(rt_renderer* r) {
         in.builder = RT_BUILDER_DEVICE;
         memcpy(rmin, res.rmin, sizeof(rmin));
         memcpy(rmax, res.rmax, sizeof(rmax));
+    }
+    {
+        // depth-K cell table over the tree (flags bits 28..31: 0 auto, 15 off, else K)
+        const uint32_t f = (r->cfg.flags >> RT_FLAG_CELL_TABLE_SHIFT) & 0xFu;
+        const uint32_t k_req = f == 0 ? kCellTableAuto : f == 15 ? kCellTableOff : f;
+        hipError_t e = r->cell_table.build(sc.nodes, sc.root, sc.root_is_leaf != 0, depth,
+                                           in.depth_reached, k_req, r->stream);
+        if (e != hipSuccess) return hip_fail(r, e, "cell table build");
+        sc.tab = r->cell_table.table();
+        sc.tab_k = r->cell_table.k();
+        in.cell_table_depth = sc.tab_k;
     }
     auto t1 = std::chrono::steady_clock::now();
     sc.spheres = r->d_spheres.p;
@@ -488,6 +500,7 @@ int rt_destroy(rt_renderer* r) {
     r->d_spheres.release();
     r->d_albedo.release();
     r->gpu_build.release();
+    r->cell_table.release();
     if (r->ev0) (void)hipEventDestroy(r->ev0);
     if (r->ev1) (void)hipEventDestroy(r->ev1);
     if (r->stream) (void)hipStreamDestroy(r->stream);

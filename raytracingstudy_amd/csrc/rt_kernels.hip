@@ -314,30 +314,78 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         // the same plane values) as the oracle's c * size forms, 3 VALU a plane.
         uint32_t depth = 0, l0 = 0, l1 = 0, l2 = 0, size = G;
         float t = t0;
+        // Cell table: the walk enters at depth K through one
+        // table load, and a step whose common ancestor lies above depth K
+        // jumps the same way instead of re-reading the records down to K.
+        const uint2* __restrict__ tab = S.tab;
+        const uint32_t K = S.tab_k;
+        bool jump = tab != nullptr;
+        uint32_t from = 0;  // depth the oracle re-descends from (stats)
         // Hard cap (never reached by a correct walk: a ray crosses < 3*G cells
         // and each crossing costs at most one descent): no input can hang the GPU.
         for (uint32_t it = 0, cap = 8u * G + 64u; it < cap; ++it) {
-            const uint32_t half = size >> 1;
-            const bool b0 = plane(0, l0 + half) <= t;
-            const bool b1 = plane(1, l1 + half) <= t;
-            const bool b2 = plane(2, l2 + half) <= t;
-            const uint32_t bits = (b0 ? 1u : 0u) | (b1 ? 2u : 0u) | (b2 ? 4u : 0u);
-            const uint32_t child = bits ^ mask;
-            l0 += b0 ? half : 0u;
-            l1 += b1 ? half : 0u;
-            l2 += b2 ? half : 0u;
-            size = half;
-            depth += 1;
-            const uint32_t valid = node.y & 0xFFu;
-            if (valid & (1u << child)) {
-                const uint32_t slot = node.x + __builtin_popcount(valid & ((1u << child) - 1u));
-                const uint2 rec = nodes[slot];
-                if (kStats) n_nodes += 1;
-                if (!((node.y >> 8) & (1u << child))) {
+            uint2 rec;
+            bool have;  // rec is a leaf record (else the cell is empty)
+            if (jump) {
+                jump = false;
+                // mid-plane tests at t from `depth` down to K (no loads: the
+                // descent's child choices), then the cell's table entry
+                while (depth < K) {
+                    const uint32_t half = size >> 1;
+                    l0 += plane(0, l0 + half) <= t ? half : 0u;
+                    l1 += plane(1, l1 + half) <= t ? half : 0u;
+                    l2 += plane(2, l2 + half) <= t ? half : 0u;
+                    size = half;
+                    depth += 1;
+                }
+                const uint32_t sh = D - K, top = (1u << K) - 1u;
+                // real cell coordinates: mirrored axes count from the far side
+                const uint32_t c0 = (mask & 1u) ? top - (l0 >> sh) : l0 >> sh;
+                const uint32_t c1 = (mask & 2u) ? top - (l1 >> sh) : l1 >> sh;
+                const uint32_t c2 = (mask & 4u) ? top - (l2 >> sh) : l2 >> sh;
+                const uint2 e = tab[(c2 << (2u * K)) | (c1 << K) | c0];
+                const uint32_t kind = e.y >> kCellKindShift;
+                depth = (e.y >> kCellDepthShift) & 31u;
+                size = G >> depth;
+                l0 &= ~(size - 1u);
+                l1 &= ~(size - 1u);
+                l2 &= ~(size - 1u);
+                rec = make_uint2(e.x, e.y & kCellRecMask);
+                // the oracle reads one record per level from `from` down to
+                // the covering node (an empty child's own level reads none)
+                if (kStats) n_nodes += (kind == kCellEmpty ? depth - 1u : depth) - from;
+                if (kind == kCellInternal) {
                     node = rec;
                     stk[(depth - 1) * kBlockThreads] = rec;
                     continue;
                 }
+                have = kind == kCellLeaf;
+            } else {
+                const uint32_t half = size >> 1;
+                const bool b0 = plane(0, l0 + half) <= t;
+                const bool b1 = plane(1, l1 + half) <= t;
+                const bool b2 = plane(2, l2 + half) <= t;
+                const uint32_t bits = (b0 ? 1u : 0u) | (b1 ? 2u : 0u) | (b2 ? 4u : 0u);
+                const uint32_t child = bits ^ mask;
+                l0 += b0 ? half : 0u;
+                l1 += b1 ? half : 0u;
+                l2 += b2 ? half : 0u;
+                size = half;
+                depth += 1;
+                const uint32_t valid = node.y & 0xFFu;
+                have = (valid & (1u << child)) != 0;
+                if (have) {
+                    const uint32_t slot = node.x + __builtin_popcount(valid & ((1u << child) - 1u));
+                    rec = nodes[slot];
+                    if (kStats) n_nodes += 1;
+                    if (!((node.y >> 8) & (1u << child))) {
+                        node = rec;
+                        stk[(depth - 1) * kBlockThreads] = rec;
+                        continue;
+                    }
+                }
+            }
+            if (have) {
                 if (leaf(rec.x, rec.y)) return true;
             }
             const float e0 = plane(0, l0 + size);
@@ -356,6 +404,26 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             if ((n0 | n1 | n2) >= G) break;  // left the root
             const uint32_t diff = (l0 ^ n0) | (l1 ^ n1) | (l2 ^ n2);
             const uint32_t top = 31u - __builtin_clz(diff);  // highest flipped bit
+            if (D - (top + 1u) < K) {
+                // the common ancestor lies above the table level: jump.  A cell
+                // at depth >= K indexes the table directly from its corner; a
+                // shallower one resolves down to K from the ancestor's cell.
+                if (depth < K) {
+                    size = 2u << top;
+                    depth = D - (top + 1u);
+                    l0 = n0 & ~(size - 1u);
+                    l1 = n1 & ~(size - 1u);
+                    l2 = n2 & ~(size - 1u);
+                } else {
+                    l0 = n0;
+                    l1 = n1;
+                    l2 = n2;
+                }
+                if (kStats) from = D - (top + 1u);
+                jump = true;
+                t = texit;
+                continue;
+            }
             // ancestor cell size = 2^(top+1); its depth = D - (top+1)
             size = 2u << top;
             const uint32_t m = depth - (D - (top + 1u));

@@ -33,6 +33,18 @@ constexpr uint32_t kOptBtsShift = 1;       // bits 1..3: force the block-tile si
                                            // 0 auto, 1 = 16, 2 = 8, 3 = 4, 4 = 2 pixels
 constexpr uint32_t kOptChunkShift = 4;     // bits 4..5: wave-queue tiles per ticket = 1 << k
 
+// Depth-K cell table (cell_table.hip): entry = {record.x, record.y (24 bits) |
+// depth << 24 | kind << 29} of the node covering each depth-K cell.
+constexpr uint32_t kCellInternal = 0;  // internal node at depth K
+constexpr uint32_t kCellLeaf = 1;      // leaf at depth <= K containing the cell
+constexpr uint32_t kCellEmpty = 2;     // empty child (depth <= K) containing the cell
+constexpr uint32_t kCellRecMask = 0xFFFFFFu;
+constexpr uint32_t kCellDepthShift = 24;
+constexpr uint32_t kCellKindShift = 29;
+constexpr uint32_t kCellTableMaxK = 7;        // 2^21 entries, 16 MiB
+constexpr uint32_t kCellTableAuto = 0xFFFFFFFFu;
+constexpr uint32_t kCellTableOff = 0;
+
 // counters[] layout: [0..3] stats, [kQueueSlot] block-tile queue head (own
 // cache line), then 8 per-XCD wave-queue heads, one per 128-byte line
 constexpr uint32_t kQueueSlot = 8;
@@ -82,6 +94,8 @@ struct SceneArgs {
     float scale[3];          // G / (rmax - rmin), f32
     float G;
     uint32_t opt;            // kOpt* toggles (A/B only; 0 = all optimisations on)
+    const uint2* tab;        // depth-tab_k cell table, or null (cell_table.hip)
+    uint32_t tab_k;          // 0: no table
 };
 
 struct FrameArgs {

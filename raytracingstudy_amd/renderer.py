@@ -106,7 +106,7 @@ class KernelRenderer:
                  shadows: bool = True, radiance: bool = False,
                  light_dir: Sequence[float] = (1.0, 1.0, -1.0), ambient: float = 0.1,
                  variant: int = 0, opt_off: int = 0, host_build: bool = False,
-                 progressive: bool = False):
+                 progressive: bool = False, cell_table: Optional[int] = None):
         lib = _lib.load()
         cfg = RtConfig()
         lib.rt_config_default(ctypes.byref(cfg))
@@ -129,7 +129,13 @@ class KernelRenderer:
         if progressive:
             flags |= RT_FLAG_PROGRESSIVE
         flags |= (int(variant) & 0xF) << _lib.RT_FLAG_VARIANT_SHIFT
-        flags |= (int(opt_off) & 0xF) << _lib.RT_FLAG_OPT_SHIFT
+        flags |= (int(opt_off) & 0xFF) << _lib.RT_FLAG_OPT_SHIFT
+        # cell_table: None = depth chosen from the tree, 0 = no table, k = depth k
+        if cell_table is not None:
+            ct = _lib.RT_CELL_TABLE_OFF if int(cell_table) == 0 else int(cell_table)
+            if not 1 <= ct <= 15:
+                raise ValueError("cell_table must be None, 0 (off) or a depth 1..7")
+            flags |= ct << _lib.RT_FLAG_CELL_TABLE_SHIFT
         cfg.flags = flags
         for i in range(3):
             cfg.light_dir[i] = float(light_dir[i])

@@ -68,22 +68,27 @@ def test_compat_reference_intrinsic_k0(gpu, oracle):
 
 
 def _scene_pair(oracle, n, w, h, spp, depth=7, pose=None, shadows=True, jitter=None, seed=rt.SEED,
-                leaf=8, spheres=None, rect=None, row_step=1, variant=0):
+                leaf=8, spheres=None, rect=None, row_step=1, variant=0, cell_table=None):
     if spheres is None:
         sp, al = rt.generate_spheres(n, rt.SEED)
     else:
         sp, al = spheres
     pose = scene_pose() if pose is None else pose
     r = rt.KernelRenderer(w, h, mode="scene", spp=spp, seed=seed, radiance=True, shadows=shadows,
-                          jitter=jitter, variant=variant)
+                          jitter=jitter, variant=variant, cell_table=cell_table)
     r.resize(w, h)
     r.setPosition(pose)
     info = r.set_scene(sp, al, max_depth=depth, leaf_capacity=leaf)
+    # plain frame first (the timed, counter-free build), then a stats frame:
+    # both must give the same image
+    r.render()
+    img_plain, rad_plain = r.readback(), r.readback_radiance()
     st = r.render(stats=True)
     img = r.readback()
     rad = r.readback_radiance()
     _, K = r.camera()
     r.close()
+    assert np.array_equal(img_plain, img) and np.array_equal(rad_plain, rad)
     sc = oracle.Scene(sp, al, max_depth=depth, leaf_capacity=leaf)
     oinfo = sc.info()
     ref8, ref32, cnt = sc.render(w, h, pose, K, spp=spp, seed=seed, jitter=jitter, shadows=shadows,
@@ -125,6 +130,27 @@ def test_scene_bit_exact(gpu, oracle, n, w, h, spp, depth, variant):
     _check_counts(st, cnt, variant)
 
 
+@pytest.mark.parametrize("cell_table", [None, 0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("n,w,h,spp,depth", [
+    (1000, 160, 120, 4, 7),
+    (20000, 200, 150, 2, 7),
+    (20000, 128, 96, 2, 12),
+    (3000, 96, 64, 64, 9),
+])
+def test_scene_cell_table(gpu, oracle, n, w, h, spp, depth, cell_table):
+    """The depth-K cell table (any K, none, or the chosen one) changes neither
+    the image nor the oracle's node/sphere counters."""
+    img, rad, st, info, ref8, ref32, cnt, _ = _scene_pair(oracle, n, w, h, spp, depth,
+                                                           cell_table=cell_table)
+    if cell_table == 0:
+        assert info["cell_table_depth"] == 0
+    elif cell_table is not None:
+        assert 1 <= info["cell_table_depth"] <= min(cell_table, depth)
+    assert np.array_equal(rad, ref32)
+    assert np.array_equal(img, ref8)
+    _check_counts(st, cnt, 0)
+
+
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_scene_c2_full_size(gpu, oracle, variant):
     """C2 at its full size: 1920x1080, 1 spp, 1k spheres."""
@@ -154,6 +180,7 @@ def test_scene_c3_full_spp_rows(gpu, oracle, variant):
     rows = np.arange(0, 1080, 64)
     assert np.array_equal(img[rows], ref8[rows])
     assert np.array_equal(rad[rows], ref32[rows])
+    assert info["cell_table_depth"] == 5  # chosen from the tree
 
 
 def test_scene_c4_rows(gpu, oracle):
@@ -171,6 +198,7 @@ def test_scene_c5_rows(gpu, oracle):
     img, rad, st, info, ref8, ref32, cnt, oinfo = _scene_pair(oracle, 1_000_000, 1920, 1080, 256,
                                                                depth=12, row_step=135)
     assert (info["n_nodes"], info["n_prim_refs"]) == (oinfo["n_nodes"], oinfo["n_prim_refs"])
+    assert info["cell_table_depth"] == 6
     rows = np.arange(0, 1080, 135)
     assert np.array_equal(img[rows], ref8[rows])
     assert np.array_equal(rad[rows], ref32[rows])

@@ -31,7 +31,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--spp", type=int, default=0, help="override spp")
     args = ap.parse_args()
-    # a variant spec is "V" or "V:OPT" (OPT = rt_config opt-off bits, A/B toggles)
+    # a variant spec is "V", "V:OPT" or "V:OPT:T" (OPT = rt_config opt bits, A/B
+    # toggles; T = cell-table depth: 0 off, 1..7, absent = chosen from the tree)
     variants = args.variants.split(",")
     out = {}
     for name in args.configs.split(","):
@@ -40,12 +41,14 @@ def main():
         sp, al = rt.generate_spheres(cfg.n_spheres, rt.SEED)
         rs = {}
         for v in variants:
-            vv, _, oo = v.partition(":")
+            vv, _, rest = v.partition(":")
+            oo, _, tt = rest.partition(":")
             r = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=spp, variant=int(vv),
-                                  opt_off=int(oo or 0))
+                                  opt_off=int(oo or 0), cell_table=int(tt) if tt else None)
             r.resize(cfg.width, cfg.height)
             r.setPosition(scene_pose())
-            r.set_scene(sp, al, max_depth=cfg.max_depth)
+            info = r.set_scene(sp, al, max_depth=cfg.max_depth)
+            r.cell_table_depth = info["cell_table_depth"]
             r.render(stats=True)  # warm-up
             rs[v] = r
         # timed frames are plain frames (no work counters), HIP events on a torch stream
@@ -73,6 +76,7 @@ def main():
                       "Mrays_s": round(rays / med / 1e3, 1), "rays": int(rays),
                       "nodes_per_ray": round(st.nodes_visited / rays, 2),
                       "prims_per_ray": round(st.prims_tested / rays, 2),
+                      "cell_table_depth": rs[v].cell_table_depth,
                       "image_equal_to_v%s" % variants[0]: bool(np.array_equal(img, ref))}
             rs[v].close()
         out[f"{name} spp{spp}"] = res
