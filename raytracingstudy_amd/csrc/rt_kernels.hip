@@ -133,6 +133,13 @@ __device__ __forceinline__ bool isect(float o0, float o1, float o2, float d0, fl
     return true;
 }
 
+// Ancestor-stack levels per thread: depths 1..D-1, or K..D-1 with a cell table
+// (a pop above depth K jumps through the table instead).
+__host__ __device__ inline uint32_t stack_levels(const SceneArgs& S) {
+    const uint32_t sb = S.tab_k ? S.tab_k - 1u : 0u;
+    return S.max_depth > 1u + sb ? S.max_depth - 1u - sb : 1u;
+}
+
 // Grid-space octree walk (DESIGN.md "Octree walk"): mirrored origin so every
 // direction component is >= 0 (the Revelles entry step of hit_sphere,
 // src/renderer.cu:23-43), cell planes at integer grid coordinates, descend by
@@ -321,6 +328,8 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         const uint32_t K = S.tab_k;
         bool jump = tab != nullptr;
         uint32_t from = 0;  // depth the oracle re-descends from (stats)
+        // with a table, only depths >= K are ever on the stack (stack_levels)
+        const uint32_t sb = K ? K - 1u : 0u;
         // Hard cap (never reached by a correct walk: a ray crosses < 3*G cells
         // and each crossing costs at most one descent): no input can hang the GPU.
         for (uint32_t it = 0, cap = 8u * G + 64u; it < cap; ++it) {
@@ -356,7 +365,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 if (kStats) n_nodes += (kind == kCellEmpty ? depth - 1u : depth) - from;
                 if (kind == kCellInternal) {
                     node = rec;
-                    stk[(depth - 1) * kBlockThreads] = rec;
+                    stk[(depth - 1 - sb) * kBlockThreads] = rec;
                     continue;
                 }
                 have = kind == kCellLeaf;
@@ -380,7 +389,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                     if (kStats) n_nodes += 1;
                     if (!((node.y >> 8) & (1u << child))) {
                         node = rec;
-                        stk[(depth - 1) * kBlockThreads] = rec;
+                        stk[(depth - 1 - sb) * kBlockThreads] = rec;
                         continue;
                     }
                 }
@@ -432,7 +441,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             l1 = n1 & ~(size - 1u);
             l2 = n2 & ~(size - 1u);
             // m == 1: the ancestor is the node we are iterating (still in `node`)
-            if (m > 1) node = depth ? stk[(depth - 1) * kBlockThreads] : S.root;
+            if (m > 1) node = depth ? stk[(depth - 1 - sb) * kBlockThreads] : S.root;
             t = texit;
         }
     }
@@ -930,8 +939,7 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
     // per-wave leaf buffer after the ancestor stacks (scene_lds_bytes)
     float4* lbuf = nullptr;
     if (kLeafMode == 1) {
-        const uint32_t levels = a.sc.max_depth > 1 ? a.sc.max_depth - 1 : 1;
-        lbuf = lds + kBlockThreads + levels * (kBlockThreads / 2) + wave * kLeafBuf;
+        lbuf = lds + kBlockThreads + stack_levels(a.sc) * (kBlockThreads / 2) + wave * kLeafBuf;
     }
     const uint32_t tw = a.tw, th = a.th;
     uint32_t n_shadow = 0, n_nodes = 0, n_prims = 0, n_primary = 0;
@@ -1058,7 +1066,7 @@ size_t scene_lds_bytes(const FrameArgs& a) {
     const size_t colours = kBlockThreads * sizeof(float4);  // pixel sums
     if (a.variant == kVariantPacket)
         return colours + static_cast<size_t>(a.stack_entries) * (kBlockThreads / 64) * sizeof(PStackEntry);
-    const uint32_t levels = a.sc.max_depth > 1 ? a.sc.max_depth - 1 : 1;
+    const uint32_t levels = stack_levels(a.sc);
     const size_t leafbuf = a.variant == kVariantWaveQLds
                                ? static_cast<size_t>(kBlockThreads / 64) * kLeafBuf * sizeof(float4)
                                : 0;
@@ -1199,12 +1207,30 @@ static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStr
                                           2>,
                              a, lds, st);
             break;
-        case kVariantWaveQ:  // per-wave scheduling over per-XCD queues
+        case kVariantWaveQ6:  // 13 at the allocator's own occupancy (6 waves/SIMD, no VGPR spills)
             if (a.count_work)
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true>,
                              a, lds, st);
             else
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true>,
+                             a, lds, st);
+            break;
+        case kVariantWaveQ8:  // 13 compiled for 8 waves/SIMD
+            if (a.count_work)
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 8, 2, true, false, true>,
+                             a, lds, st);
+            else
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 8, 2, false, false, true>,
+                             a, lds, st);
+            break;
+        case kVariantWaveQ:  // per-wave scheduling over per-XCD queues, 7 waves/SIMD
+            // (72 VGPRs; the few VGPR spills are per pixel, outside the walk
+            // loop: C3 -2.8%, C5 -5.4% against 6 waves, profiles/r01/occupancy_ab.log)
+            if (a.count_work)
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, true, false, true>,
+                             a, lds, st);
+            else
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, false, false, true>,
                              a, lds, st);
             break;
         case kVariantLaneUnified2NoStats:  // A/B only: variant 7 without the work counters

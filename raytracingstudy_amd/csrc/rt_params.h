@@ -21,11 +21,13 @@ constexpr uint32_t kVariantLaneChunk2 = 3;  // lane walk, 2 leaf spheres in flig
 constexpr uint32_t kVariantLaneUnified = 7;   // one walk instance for primary + shadow, 2 in flight
 constexpr uint32_t kVariantLaneUnified2NoStats = 10; // A/B: 7 with counters only in stats frames
 constexpr uint32_t kVariantWaveQ = 13;     // unified walk scheduled per wave over per-XCD queues
-                                           // (default for spp >= 8)
+                                           // (default for spp >= 8), 7 waves/SIMD
 constexpr uint32_t kVariantWaveQLds = 14;  // 13 + wave-uniform leaves fetched once into LDS
 constexpr uint32_t kLeafBuf = 16;          // spheres per wave in the LDS leaf buffer
 constexpr uint32_t kVariantWaveQSmem = 15; // 13 + wave-uniform leaves read by scalar loads
 constexpr uint32_t kVariantWaveQLane = 16; // 13 + one-lane leaf loads, readfirstlane broadcast
+constexpr uint32_t kVariantWaveQ6 = 8;     // 13 at 6 waves/SIMD, no spills (A/B)
+constexpr uint32_t kVariantWaveQ8 = 9;     // 13 compiled for 8 waves/SIMD (A/B)
 constexpr uint32_t kPrimPad = 4;           // prim_sp padding: scalar reads may run 3 past a leaf
 
 // A/B toggles (rt_config.flags bits 20..23), results identical either way

@@ -98,7 +98,7 @@ def _scene_pair(oracle, n, w, h, spp, depth=7, pose=None, shadows=True, jitter=N
 
 # 0 = the library default; 1 lane walk; 2 wave packets; 3 lane walk, 2 spheres in
 # flight; 7 unified primary+shadow walk; 10 unified, counters only in stats frames
-VARIANTS = [0, rt._lib.VARIANT_LANE, rt._lib.VARIANT_PACKET, 3, 7, 10, 13, 14, 15, 16]
+VARIANTS = [0, rt._lib.VARIANT_LANE, rt._lib.VARIANT_PACKET, 3, 7, 8, 9, 10, 13, 14, 15, 16]
 
 
 def _check_counts(st, cnt, variant):

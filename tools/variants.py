@@ -34,6 +34,8 @@ def main():
     # a variant spec is "V", "V:OPT" or "V:OPT:T" (OPT = rt_config opt bits, A/B
     # toggles; T = cell-table depth: 0 off, 1..7, absent = chosen from the tree)
     variants = args.variants.split(",")
+    if len(set(variants)) != len(variants):
+        ap.error("--variants: each spec at most once (rounds repeat them)")
     out = {}
     for name in args.configs.split(","):
         cfg = rt.CONFIGS[name]
