@@ -98,6 +98,36 @@ def cpu_baseline(cfg, K, pose, target_s: float) -> dict:
                             "sample": f"every {s1}th row ({rays1} rays) in {el1:.2f} s"}}
 
 
+def pmc_figures(path: str, cfg_name: str, world: int, kern_ms: float, simds: int):
+    """(HBM bytes per launch, VALU-issue roofline dict) from the committed PMC
+    summary (tools/pmc_traffic.py output: one flat object naming its config),
+    or (None, None) when it is missing or was taken on another config."""
+    try:
+        with open(path) as f:
+            pm = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    ent = pm if pm.get("config") == cfg_name else pm.get(cfg_name)
+    if not isinstance(ent, dict) or ent.get("n_gpus", 1) != world:
+        return None, None
+    traffic = ent.get("hbm_bytes_per_launch")
+    insts = ent.get("valu_insts_per_launch", ent.get("sq", {}).get("SQ_INSTS_VALU"))
+    clock = ent.get("clock_ghz", ent.get("effective_clock_ghz"))
+    if not (insts and clock):
+        return traffic, None
+    # what bounds this kernel: VALU issue (a wave64 VALU instruction occupies a
+    # SIMD-32 for 2 cycles, MI355X_MICROARCH.md), with the PMC instruction count
+    # over the live kernel time
+    peak = simds * clock * 1e9 / 2.0
+    rate = insts / (kern_ms / 1e3)
+    valu = {"insts_per_launch": insts, "achieved_winst_per_s": round(rate / 1e9, 2),
+            "peak_winst_per_s": round(peak / 1e9, 2), "unit": "G wave-instr/s",
+            "frac": round(rate / peak, 4), "clock_ghz": round(clock, 4),
+            "source": "rocprofv3 --pmc SQ_INSTS_VALU, GRBM_GUI_ACTIVE "
+                      f"({os.path.relpath(path, ROOT)})"}
+    return traffic, valu
+
+
 def secondary_config(rt, torch, name: str, dev, stream, steps: int = 3) -> dict:
     """Time another BASELINE config on this GPU: kernel ms (HIP events on the
     launch stream), Mrays/s from the counted rays, scene build time."""
@@ -249,29 +279,8 @@ def main():
         pix = (W * H) if not tiled else len(my_ids) * ts * ts
         alg_bytes = float(cnt[2].item()) * NODE_BYTES + float(cnt[3].item()) * PRIM_BYTES + pix * PIXEL_BYTES
         achieved = alg_bytes / (kern_ms / 1e3) / 1e9
-        traffic = None
-        valu = None
-        try:
-            with open(args.pmc) as f:
-                pm = json.load(f)
-            ent = pm.get(cfg.name)
-            if ent and ent.get("n_gpus", 1) == world:
-                traffic = ent.get("hbm_bytes_per_launch")
-                if ent.get("valu_insts_per_launch") and ent.get("clock_ghz"):
-                    # what bounds this kernel: VALU issue (a wave64 VALU instruction
-                    # occupies a SIMD-32 for 2 cycles, MI355X_MICROARCH.md), with the
-                    # PMC instruction count over the live kernel time
-                    simds = torch.cuda.get_device_properties(dev).multi_processor_count * 4
-                    peak = simds * ent["clock_ghz"] * 1e9 / 2.0
-                    rate = ent["valu_insts_per_launch"] / (kern_ms / 1e3)
-                    valu = {"insts_per_launch": ent["valu_insts_per_launch"],
-                            "achieved_winst_per_s": round(rate / 1e9, 2),
-                            "peak_winst_per_s": round(peak / 1e9, 2), "unit": "G wave-instr/s",
-                            "frac": round(rate / peak, 4), "clock_ghz": ent["clock_ghz"],
-                            "source": "rocprofv3 --pmc SQ_INSTS_VALU, GRBM_GUI_ACTIVE "
-                                      "(profiles/r01/pmc_summary.json)"}
-        except (OSError, ValueError):
-            pass
+        simds = torch.cuda.get_device_properties(dev).multi_processor_count * 4
+        traffic, valu = pmc_figures(args.pmc, cfg.name, world, kern_ms, simds)
         out = {
             "metric": f"Mrays/s (primary+shadow) at {W}x{H}, {cfg.spp} spp, {cfg.n_spheres} spheres",
             "value": round(value, 3),

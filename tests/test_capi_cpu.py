@@ -129,3 +129,16 @@ def test_gl_interop_header_compiles(tmp_path):
                         os.path.join(ROOT, "tests", "native", "gl_interop_use.cpp")],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_committed_pmc_summary_feeds_the_bench_roofline():
+    """bench.py reads profiles/pmc_latest.json (tools/pmc_traffic.py output) for
+    `roofline.traffic` and `roofline.valu_issue`; a format drift would silently
+    null them in the round-end bench line."""
+    import bench
+    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    traffic, valu = bench.pmc_figures(path, "c3", 1, 13.5, 1024)
+    assert traffic and traffic > 0
+    assert valu and 0.0 < valu["frac"] < 1.0
+    assert bench.pmc_figures(path, "c5", 1, 13.5, 1024) == (None, None)
+    assert bench.pmc_figures(path, "c3", 2, 13.5, 1024) == (None, None)
