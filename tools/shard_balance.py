@@ -46,6 +46,8 @@ def main():
     stream = torch.cuda.Stream()
 
     def timed(fn):
+        fn()  # two untimed frames: the heavy-first list of this tile list is live
+        fn()
         ts = []
         for _ in range(args.rounds):
             e0 = torch.cuda.Event(enable_timing=True)
