@@ -355,8 +355,31 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     RT_HIP(r, hipMemsetAsync(r->counters.p, 0, kCounterWords * sizeof(unsigned long long), st));
     a.count_work = stats ? 1u : 0u;
     if (stats) RT_HIP(r, hipEventRecord(r->ev0, st));
+#ifdef RT_TIMELINE
+    // diagnostic build (tools/timeline.sh): every stats frame appends its
+    // per-wave timeline to $RT_TIMELINE_FILE
+    static unsigned long long* tl = nullptr;
+    const size_t tl_waves = 1u << 16;
+    const char* tl_file = getenv("RT_TIMELINE_FILE");
+    if (tl_file) {
+        if (!tl) RT_HIP(r, hipMalloc(reinterpret_cast<void**>(&tl), tl_waves * 32));
+        RT_HIP(r, hipMemsetAsync(tl, 0, tl_waves * 32, st));
+        a.timeline = tl;
+    }
+#endif
     hipError_t e = r->cfg.mode == RT_MODE_SCENE ? launch_scene(a, st) : launch_compat(a, st);
     if (e != hipSuccess) return hip_fail(r, e, "kernel launch");
+#ifdef RT_TIMELINE
+    if (tl_file) {
+        std::vector<unsigned long long> h(tl_waves * 4);
+        RT_HIP(r, hipStreamSynchronize(st));
+        RT_HIP(r, hipMemcpy(h.data(), tl, tl_waves * 32, hipMemcpyDeviceToHost));
+        if (FILE* f = fopen(tl_file, "ab")) {
+            fwrite(h.data(), 8, h.size(), f);
+            fclose(f);
+        }
+    }
+#endif
     if (a.accum) ++r->frames_accum;
     if (stats) {
         RT_HIP(r, hipEventRecord(r->ev1, st));

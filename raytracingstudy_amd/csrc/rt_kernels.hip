@@ -943,19 +943,28 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
     }
     const uint32_t tw = a.tw, th = a.th;
     uint32_t n_shadow = 0, n_nodes = 0, n_prims = 0, n_primary = 0;
+#ifdef RT_TIMELINE
+    // diagnostic build only (tools/timeline.sh): per-wave {start, first empty
+    // range, exit, units} in wall-clock ticks
+    const unsigned long long tl_start = wall_clock64();
+    unsigned long long tl_empty = 0, tl_units = 0;
+#endif
     if (kWaveQ) {
         // wave-tile grid of the frame, or of one packed tile
         const uint32_t gw = kTiles ? a.tile_size / tw : (a.W + tw - 1) / tw;
         const uint32_t gh = kTiles ? a.tile_size / th : (a.H + th - 1) / th;
         const uint32_t nbx = (gw + 7u) / 8u, nby = (gh + 7u) / 8u;
-        const uint32_t per_grid = nbx * nby;  // 8x8-wave-tile blocks per grid
-        const uint32_t n_blocks = kTiles ? a.n_tiles * per_grid : per_grid;
+        // superblock = 8x8 blocks of 8x8 wave tiles (one 64x64 tile at 64 spp)
+        const uint32_t nsx = (nbx + 7u) / 8u, nsy = (nby + 7u) / 8u;
+        const uint32_t sb_grid = nsx * nsy;  // superblocks per grid
+        const uint32_t n_sb = kTiles ? a.n_tiles * sb_grid : sb_grid;
         const uint32_t grp = blockIdx.x & 7u;
         for (uint32_t hop = 0; hop < 8u; ++hop) {
             const uint32_t q = (grp + hop) & 7u;
-            // range q = whole blocks [n_blocks*q/8, n_blocks*(q+1)/8), 64 units each
-            const uint32_t lo = 64u * static_cast<uint32_t>((uint64_t)n_blocks * q / 8u);
-            const uint32_t hi = 64u * static_cast<uint32_t>((uint64_t)n_blocks * (q + 1u) / 8u);
+            // range q = superblocks q, q + 8, q + 16, ... (4096 units each):
+            // every XCD's share is spread over the whole image, so the ranges
+            // cost about the same and stealing is left to the very end
+            const uint32_t hi = (n_sb > q ? (n_sb - q + 7u) / 8u : 0u) * 4096u;
             unsigned long long* head = a.counters + kWaveQueueBase + q * kWaveQueueStride;
             const uint32_t chunk = a.wq_chunk;  // wave tiles per ticket
             uint32_t u = hi, u_end = hi;
@@ -963,20 +972,23 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
                 if (u >= u_end) {  // take the next ticket
                     uint32_t t = 0;
                     if ((threadIdx.x & 63u) == 0) t = static_cast<uint32_t>(atomicAdd(head, 1ull));
-                    u = lo + __builtin_amdgcn_readfirstlane(t) * chunk;
+                    u = __builtin_amdgcn_readfirstlane(t) * chunk;
+#ifdef RT_TIMELINE
+                    if (u >= hi && !tl_empty) tl_empty = wall_clock64();
+#endif
                     if (u >= hi) break;
                     u_end = min(u + chunk, hi);
                 }
                 const uint32_t cur = u++;
-                const uint32_t bidx = cur >> 6, w = cur & 63u;
-                uint32_t k = 0, blk = bidx;
+                const uint32_t sb = q + 8u * (cur >> 12), b = (cur >> 6) & 63u, w = cur & 63u;
+                uint32_t k = 0, sg = sb;
                 if (kTiles) {
-                    k = bidx / per_grid;
-                    blk = bidx - k * per_grid;
+                    k = sb / sb_grid;
+                    sg = sb - k * sb_grid;
                 }
-                const uint32_t wx = (blk % nbx) * 8u + (w & 7u);
-                const uint32_t wy = (blk / nbx) * 8u + (w >> 3);
-                if (wx >= gw || wy >= gh) continue;  // padding of an edge block
+                const uint32_t wx = ((sg % nsx) * 8u + (b & 7u)) * 8u + (w & 7u);
+                const uint32_t wy = ((sg / nsx) * 8u + (b >> 3)) * 8u + (w >> 3);
+                if (wx >= gw || wy >= gh) continue;  // padding of an edge superblock
                 const uint32_t olx = wx * tw, oly = wy * th;
                 uint32_t ox = olx, oy = oly;
                 if (kTiles) {
@@ -1025,6 +1037,16 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
         }
     }
     flush_counters(a, n_primary, n_shadow, n_nodes, n_prims);
+#ifdef RT_TIMELINE
+    tl_units = n_primary;
+    if (a.timeline && (threadIdx.x & 63u) == 0) {
+        unsigned long long* e = a.timeline + 4ull * (blockIdx.x * (kBlockThreads / 64) + wave);
+        e[0] = tl_start;
+        e[1] = tl_empty;
+        e[2] = wall_clock64();
+        e[3] = tl_units;
+    }
+#endif
 }
 
 __global__ void __launch_bounds__(kBlockThreads)

@@ -131,6 +131,9 @@ struct FrameArgs {
     uint32_t count_work;  // 1: also count node visits / sphere tests (stats frames)
     uint32_t bts;         // block-tile side in pixels (set by the launcher)
     uint32_t wq_chunk;    // wave-queue scheduling: wave tiles per dequeue ticket
+#ifdef RT_TIMELINE
+    unsigned long long* timeline;  // diagnostic build: 4 words per wave
+#endif
 };
 
 }  // namespace rtamd

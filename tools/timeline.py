@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Per-wave timeline of the wave-queue scene kernel (diagnostic build).
+
+    bash tools/build_flags.sh timeline -DRT_TIMELINE
+    RT_AMD_LIB=build_ab/librt_timeline.so python tools/timeline.py [--config c3] [--n 8]
+
+Renders the full frame and rank 0's N-way share a few times; every frame's
+per-wave {start, first empty range, exit, units} (100 MHz wall clock) is
+summarised: the span, when the queues first ran dry, how long the last waves
+ran after that, and how many waves were still busy over the tail.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+import raytracingstudy_amd as rt  # noqa: E402
+from raytracingstudy_amd import tiles as T  # noqa: E402
+from raytracingstudy_amd.camera import scene_pose  # noqa: E402
+
+
+def summarise(rec: np.ndarray) -> dict:
+    rec = rec[rec[:, 2] > 0]
+    t0 = rec[:, 0].min()
+    start, empty, end, units = [(rec[:, i] - (t0 if i < 3 else 0)) / (100.0 if i < 3 else 1)
+                                for i in range(4)]  # us
+    empty = np.where(rec[:, 1] > 0, empty, end)
+    first_dry = float(empty.min())
+    span = float(end.max())
+    busy = lambda t: int(((start <= t) & (end > t)).sum())  # noqa: E731
+    return {"waves": int(len(rec)), "span_us": round(span, 1),
+            "start_spread_us": round(float(start.max()), 1),
+            "first_dry_us": round(first_dry, 1),
+            "end_pcts_us": [round(float(np.percentile(end, p)), 1) for p in (1, 10, 50, 90, 99, 100)],
+            "tail_us": round(span - first_dry, 1),
+            "busy_at": {f"{f:.2f}": busy(f * span) for f in (0.5, 0.8, 0.9, 0.95, 0.98)},
+            "units_per_wave": [int(units.min()), float(round(units.mean(), 1)), int(units.max())],
+            "mean_unit_us": round(float((end - start).sum() / max(units.sum(), 1)), 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--n", type=int, default=8)
+    ap.add_argument("--frames", type=int, default=3)
+    args = ap.parse_args()
+    fd, path = tempfile.mkstemp(suffix=".tl")
+    os.close(fd)
+    os.environ["RT_TIMELINE_FILE"] = path
+    import torch
+    cfg = rt.CONFIGS[args.config]
+    sp, al = rt.generate_spheres(cfg.n_spheres, rt.SEED)
+    r = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=cfg.spp)
+    r.resize(cfg.width, cfg.height)
+    r.setPosition(scene_pose())
+    r.set_scene(sp, al, max_depth=cfg.max_depth)
+    ts = rt.configs.TILE_SIZE
+    share = T.tiles_for_rank(cfg.width, cfg.height, 0, args.n, ts)
+    slab = torch.zeros(len(share) * ts * ts * 4, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    out = {}
+    for name, fn in (("full", lambda: r.render()),
+                     (f"share_1_of_{args.n}", lambda: r.render_tiles(share, ts, slab.data_ptr()))):
+        fn()  # warm-up
+        open(path, "wb").close()
+        for _ in range(args.frames):
+            fn()
+        r.synchronize()
+        raw = np.fromfile(path, dtype=np.uint64).reshape(args.frames, -1, 4).astype(np.int64)
+        out[name] = [summarise(raw[i]) for i in range(args.frames)]
+        print(name, json.dumps(out[name][-1]), flush=True)
+    os.unlink(path)
+    r.close()
+
+
+if __name__ == "__main__":
+    main()
