@@ -360,10 +360,11 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     // per-wave timeline to $RT_TIMELINE_FILE
     static unsigned long long* tl = nullptr;
     const size_t tl_waves = 1u << 16;
+    const size_t tl_words = tl_waves * 4 + (2u << 22);  // per wave, then per unit
     const char* tl_file = getenv("RT_TIMELINE_FILE");
     if (tl_file) {
-        if (!tl) RT_HIP(r, hipMalloc(reinterpret_cast<void**>(&tl), tl_waves * 32));
-        RT_HIP(r, hipMemsetAsync(tl, 0, tl_waves * 32, st));
+        if (!tl) RT_HIP(r, hipMalloc(reinterpret_cast<void**>(&tl), tl_words * 8));
+        RT_HIP(r, hipMemsetAsync(tl, 0, tl_words * 8, st));
         a.timeline = tl;
     }
 #endif
@@ -371,9 +372,9 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     if (e != hipSuccess) return hip_fail(r, e, "kernel launch");
 #ifdef RT_TIMELINE
     if (tl_file) {
-        std::vector<unsigned long long> h(tl_waves * 4);
+        std::vector<unsigned long long> h(tl_words);
         RT_HIP(r, hipStreamSynchronize(st));
-        RT_HIP(r, hipMemcpy(h.data(), tl, tl_waves * 32, hipMemcpyDeviceToHost));
+        RT_HIP(r, hipMemcpy(h.data(), tl, tl_words * 8, hipMemcpyDeviceToHost));
         if (FILE* f = fopen(tl_file, "ab")) {
             fwrite(h.data(), 8, h.size(), f);
             fclose(f);

@@ -996,8 +996,19 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
                     ox += (tile % a.tiles_x) * a.tile_size;
                     oy += (tile / a.tiles_x) * a.tile_size;
                 }
+#ifdef RT_TIMELINE
+                const unsigned long long tu0 = wall_clock64();
+#endif
                 shade_wave_tile<kTiles, kVar, kChunk, kStats, kProg, kLeafMode>(
                     a, acc, stk, lbuf, ox, oy, k, olx, oly, n_primary, n_shadow, n_nodes, n_prims);
+#ifdef RT_TIMELINE
+                // per unit {start, end} after the 65536 per-wave records
+                const unsigned long long uid = (unsigned long long)sb * 4096u + (cur & 4095u);
+                if (a.timeline && (threadIdx.x & 63u) == 0 && uid < (1ull << 22)) {
+                    a.timeline[4ull * 65536 + 2 * uid] = tu0;
+                    a.timeline[4ull * 65536 + 2 * uid + 1] = wall_clock64();
+                }
+#endif
             }
         }
     } else {

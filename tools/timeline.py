@@ -27,7 +27,29 @@ from raytracingstudy_amd import tiles as T  # noqa: E402
 from raytracingstudy_amd.camera import scene_pose  # noqa: E402
 
 
-def summarise(rec: np.ndarray) -> dict:
+WAVE_WORDS = 65536 * 4
+
+
+def summarise_units(u: np.ndarray, t0: int, span_us: float) -> dict:
+    u = u[u[:, 1] > 0]
+    st = (u[:, 0] - t0) / 100.0
+    du = (u[:, 1] - u[:, 0]) / 100.0
+    en = st + du
+    dec = np.minimum((st / span_us * 10).astype(int), 9)
+    late = en > 0.9 * span_us
+    return {"units": int(len(u)),
+            "dur_us": {p: round(float(np.percentile(du, q)), 1)
+                       for p, q in (("p50", 50), ("p90", 90), ("p99", 99), ("p99.9", 99.9))},
+            "dur_max_us": round(float(du.max()), 1), "dur_mean_us": round(float(du.mean()), 2),
+            "mean_dur_by_start_decile": [round(float(du[dec == i].mean()), 1) if (dec == i).any()
+                                         else None for i in range(10)],
+            "units_ending_last_10pct": int(late.sum()),
+            "their_dur_p50_max_us": [round(float(np.median(du[late])), 1) if late.any() else 0,
+                                     round(float(du[late].max()), 1) if late.any() else 0],
+            "their_start_min_us": round(float(st[late].min()), 1) if late.any() else 0}
+
+
+def summarise(rec: np.ndarray, unit_rec: np.ndarray) -> dict:
     rec = rec[rec[:, 2] > 0]
     t0 = rec[:, 0].min()
     start, empty, end, units = [(rec[:, i] - (t0 if i < 3 else 0)) / (100.0 if i < 3 else 1)
@@ -43,14 +65,15 @@ def summarise(rec: np.ndarray) -> dict:
             "tail_us": round(span - first_dry, 1),
             "busy_at": {f"{f:.2f}": busy(f * span) for f in (0.5, 0.8, 0.9, 0.95, 0.98)},
             "units_per_wave": [int(units.min()), float(round(units.mean(), 1)), int(units.max())],
-            "mean_unit_us": round(float((end - start).sum() / max(units.sum(), 1)), 2)}
+            "mean_unit_us": round(float((end - start).sum() / max(units.sum(), 1)), 2),
+            "unit_level": summarise_units(unit_rec, int(t0), span)}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
     ap.add_argument("--n", type=int, default=8)
-    ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=2)
     args = ap.parse_args()
     fd, path = tempfile.mkstemp(suffix=".tl")
     os.close(fd)
@@ -74,8 +97,9 @@ def main():
         for _ in range(args.frames):
             fn()
         r.synchronize()
-        raw = np.fromfile(path, dtype=np.uint64).reshape(args.frames, -1, 4).astype(np.int64)
-        out[name] = [summarise(raw[i]) for i in range(args.frames)]
+        raw = np.fromfile(path, dtype=np.uint64).reshape(args.frames, -1).astype(np.int64)
+        out[name] = [summarise(raw[i, :WAVE_WORDS].reshape(-1, 4), raw[i, WAVE_WORDS:].reshape(-1, 2))
+                     for i in range(args.frames)]
         print(name, json.dumps(out[name][-1]), flush=True)
     os.unlink(path)
     r.close()
