@@ -39,7 +39,8 @@ def summarise_units(u: np.ndarray, t0: int, span_us: float) -> dict:
     late = en > 0.9 * span_us
     return {"units": int(len(u)),
             "dur_us": {p: round(float(np.percentile(du, q)), 1)
-                       for p, q in (("p50", 50), ("p90", 90), ("p99", 99), ("p99.9", 99.9))},
+                       for p, q in (("p0.1", 0.1), ("p1", 1), ("p10", 10), ("p50", 50), ("p90", 90),
+                                    ("p99", 99), ("p99.9", 99.9))},
             "dur_max_us": round(float(du.max()), 1), "dur_mean_us": round(float(du.mean()), 2),
             "mean_dur_by_start_decile": [round(float(du[dec == i].mean()), 1) if (dec == i).any()
                                          else None for i in range(10)],
