@@ -30,6 +30,7 @@ NODE_BYTES = 8     # uint2 node record
 PRIM_BYTES = 16    # float4 sphere record per ray-sphere test
 PIXEL_BYTES = 4    # RGBA8 framebuffer write
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s over the 8 XCDs
 
 
 def parse():
@@ -317,6 +318,11 @@ def main():
                 "per_ray": {"nodes": float(cnt[2].item()) / float(cnt[0].item() + cnt[1].item()),
                             "prims": float(cnt[3].item()) / float(cnt[0].item() + cnt[1].item())},
                 "valu_issue": valu,
+                # where the touched bytes are actually served from: the same
+                # algorithmic bytes against the L2s' aggregate bandwidth
+                "l2": {"peak": L2_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(achieved / L2_PEAK_GBS, 4),
+                       "source": "MI355X_MICROARCH.md L2 (per XCD): ~34.5 TB/s aggregate"},
             },
             "cpu_baseline": None,
         }
