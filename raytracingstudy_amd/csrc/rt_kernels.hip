@@ -1079,10 +1079,6 @@ __global__ void __launch_bounds__(kBlockThreads)
 // launchers (called from rt_capi.cpp)
 // ---------------------------------------------------------------------------
 
-// ---------------------------------------------------------------------------
-// launchers (called from rt_capi.cpp)
-// ---------------------------------------------------------------------------
-
 hipError_t launch_compat(const FrameArgs& a, hipStream_t st) {
     if (a.tiles) {
         const uint32_t strips = a.tile_size / 4u * (a.tile_size / 64u);
