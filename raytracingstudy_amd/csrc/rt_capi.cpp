@@ -165,7 +165,6 @@ void fill_frame_args(rt_renderer* r, FrameArgs& a) {
     }
     a.counters = r->counters.p;
     a.sc.opt = (r->cfg.flags >> RT_FLAG_OPT_SHIFT) & 0xFFu;
-    a.wq_chunk = 1u << ((a.sc.opt >> kOptChunkShift) & 3u);
     const uint32_t v = (r->cfg.flags >> RT_FLAG_VARIANT_SHIFT) & 0xFu;
     // default: multi-sample frames are scheduled per wave over per-XCD queues
     // (variant 13: C5 -15%, equal on C3, better on multi-GPU shares); 1-spp
@@ -360,7 +359,7 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     // per-wave timeline to $RT_TIMELINE_FILE
     static unsigned long long* tl = nullptr;
     const size_t tl_waves = 1u << 16;
-    const size_t tl_words = tl_waves * 4 + (2u << 22);  // per wave, then per unit
+    const size_t tl_words = tl_waves * 4 + (2u << 22) + tl_waves * 2;  // per wave, per unit, phases
     const char* tl_file = getenv("RT_TIMELINE_FILE");
     if (tl_file) {
         if (!tl) RT_HIP(r, hipMalloc(reinterpret_cast<void**>(&tl), tl_words * 8));

@@ -253,9 +253,11 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             const uint32_t ucnt = __builtin_amdgcn_readfirstlane(cnt);
             if (__all(off == uoff)) {
                 const uint32_t lane_id = __lane_id();
-                const uint32_t first = __builtin_amdgcn_readfirstlane(lane_id);
                 const float4* __restrict__ ps = prim_sp + uoff;
                 for (uint32_t j = 0; j < ucnt; j += 2) {
+                    // the loader is the first lane still testing (any-hit lanes
+                    // leave the loop as soon as they hit)
+                    const uint32_t first = __builtin_amdgcn_readfirstlane(lane_id);
                     float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
                     if (lane_id == first) {
                         a0 = ps[j];
@@ -1282,6 +1284,12 @@ hipError_t launch_scene(const FrameArgs& a_in, hipStream_t st) {
     // wave mapping: spw samples x ppw pixels per wave (see scene_kernel)
     wave_tile_shape(a.spp, a.spw, a.g, a.ppw, a.tw, a.th);
     a.rounds = (a.spp + a.spw - 1) / a.spw;
+    // wave-queue ticket size: adjacent wave tiles back to back on one wave
+    // reuse its CU's L1; a ticket of about four rounds of work balances that
+    // against the queue tail (C3, 1 round: 4 per ticket -4.1%; C5, 4 rounds:
+    // 1 per ticket, more is slower; profiles/r01/chunk_ab.log)
+    const uint32_t ck = (a.sc.opt >> kOptChunkShift) & 7u;
+    a.wq_chunk = ck ? 1u << (ck - 1u) : std::max(1u, 4u / std::max(1u, std::min(a.rounds, 4u)));
     a.stack_entries = 8u * a.sc.max_depth + 8u;
     const size_t lds = scene_lds_bytes(a);
     if (a.tiles)

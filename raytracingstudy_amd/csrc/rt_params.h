@@ -25,7 +25,7 @@ constexpr uint32_t kVariantWaveQ = 13;     // unified walk scheduled per wave ov
 constexpr uint32_t kVariantWaveQLds = 14;  // 13 + wave-uniform leaves fetched once into LDS
 constexpr uint32_t kLeafBuf = 16;          // spheres per wave in the LDS leaf buffer
 constexpr uint32_t kVariantWaveQSmem = 15; // 13 + wave-uniform leaves read by scalar loads
-constexpr uint32_t kVariantWaveQLane = 16; // 13 + one-lane leaf loads, readfirstlane broadcast
+constexpr uint32_t kVariantWaveQLane = 12; // 13 + one-lane leaf loads, readfirstlane broadcast
 constexpr uint32_t kVariantWaveQ6 = 8;     // 13 at 6 waves/SIMD, no spills (A/B)
 constexpr uint32_t kVariantWaveQ8 = 9;     // 13 compiled for 8 waves/SIMD (A/B)
 constexpr uint32_t kPrimPad = 4;           // prim_sp padding: scalar reads may run 3 past a leaf
@@ -33,7 +33,8 @@ constexpr uint32_t kPrimPad = 4;           // prim_sp padding: scalar reads may 
 // A/B toggles (rt_config.flags bits 20..23), results identical either way
 constexpr uint32_t kOptBtsShift = 1;       // bits 1..3: force the block-tile side (A/B):
                                            // 0 auto, 1 = 16, 2 = 8, 3 = 4, 4 = 2 pixels
-constexpr uint32_t kOptChunkShift = 4;     // bits 4..5: wave-queue tiles per ticket = 1 << k
+constexpr uint32_t kOptChunkShift = 4;     // bits 4..6: wave-queue tiles per ticket: 0 auto
+                                           // (4 / rounds, at least 1), k = 1..4 -> 1 << (k - 1)
 
 // Depth-K cell table (cell_table.hip): entry = {record.x, record.y (24 bits) |
 // depth << 24 | kind << 29} of the node covering each depth-K cell.
@@ -130,7 +131,7 @@ struct FrameArgs {
     uint32_t spw, g, ppw, tw, th, rounds;  // g = pow2ceil(spw) lanes per pixel
     uint32_t count_work;  // 1: also count node visits / sphere tests (stats frames)
     uint32_t bts;         // block-tile side in pixels (set by the launcher)
-    uint32_t wq_chunk;    // wave-queue scheduling: wave tiles per dequeue ticket
+    uint32_t wq_chunk;    // wave-queue scheduling: wave tiles per dequeue ticket (launch_scene)
 #ifdef RT_TIMELINE
     unsigned long long* timeline;  // diagnostic build: 4 words per wave
 #endif

@@ -98,7 +98,7 @@ def _scene_pair(oracle, n, w, h, spp, depth=7, pose=None, shadows=True, jitter=N
 
 # 0 = the library default; 1 lane walk; 2 wave packets; 3 lane walk, 2 spheres in
 # flight; 7 unified primary+shadow walk; 10 unified, counters only in stats frames
-VARIANTS = [0, rt._lib.VARIANT_LANE, rt._lib.VARIANT_PACKET, 3, 7, 8, 9, 10, 13, 14, 15, 16]
+VARIANTS = [0, rt._lib.VARIANT_LANE, rt._lib.VARIANT_PACKET, 3, 7, 8, 9, 10, 12, 13, 14, 15]
 
 
 def _check_counts(st, cnt, variant):
@@ -393,3 +393,23 @@ def test_scene_8k_frame_rows(gpu, oracle):
     assert np.array_equal(img[rows], ref8[rows])
     assert np.array_equal(rad[rows], ref32[rows])
     assert st.primary_rays == 8192 * 4320
+
+
+@pytest.mark.parametrize("chunk_bits", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("n,w,h,spp", [(20000, 97, 61, 64), (20000, 64, 40, 128), (5000, 50, 30, 100)])
+def test_wave_queue_ticket_sizes(gpu, oracle, n, w, h, spp, chunk_bits):
+    """Wave-queue tickets of 1, 2, 4 or 8 wave tiles (opt bits 4..6; 0 = auto,
+    DESIGN.md 5.1) only change which wave renders which pixel: images and
+    counters equal the oracle's at odd sizes, where ranges end mid-ticket."""
+    sp, al = rt.generate_spheres(n, rt.SEED)
+    with rt.KernelRenderer(w, h, mode="scene", spp=spp, opt_off=chunk_bits << 4, radiance=True) as r:
+        r.resize(w, h)
+        r.setPosition(scene_pose())
+        r.set_scene(sp, al)
+        r.render()
+        img, rad = r.readback(), r.readback_radiance()
+        st = r.render(stats=True)
+        _, K = r.camera()
+    ref8, ref32, cnt = oracle.Scene(sp, al).render(w, h, scene_pose(), K, spp=spp)
+    assert np.array_equal(img, ref8) and np.array_equal(rad, ref32)
+    _check_counts(st, cnt, 0)

@@ -32,6 +32,8 @@ WAVE_WORDS = 65536 * 4
 
 def summarise_units(u: np.ndarray, t0: int, span_us: float) -> dict:
     u = u[u[:, 1] > 0]
+    if not len(u):
+        return {"units": 0}  # this path records no per-unit times
     st = (u[:, 0] - t0) / 100.0
     du = (u[:, 1] - u[:, 0]) / 100.0
     en = st + du
@@ -75,6 +77,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--n", type=int, default=8)
     ap.add_argument("--frames", type=int, default=2)
+    ap.add_argument("--variant", type=int, default=0)
     args = ap.parse_args()
     fd, path = tempfile.mkstemp(suffix=".tl")
     os.close(fd)
@@ -82,7 +85,7 @@ def main():
     import torch
     cfg = rt.CONFIGS[args.config]
     sp, al = rt.generate_spheres(cfg.n_spheres, rt.SEED)
-    r = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=cfg.spp)
+    r = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=cfg.spp, variant=args.variant)
     r.resize(cfg.width, cfg.height)
     r.setPosition(scene_pose())
     r.set_scene(sp, al, max_depth=cfg.max_depth)
@@ -99,8 +102,14 @@ def main():
             fn()
         r.synchronize()
         raw = np.fromfile(path, dtype=np.uint64).reshape(args.frames, -1).astype(np.int64)
-        out[name] = [summarise(raw[i, :WAVE_WORDS].reshape(-1, 4), raw[i, WAVE_WORDS:].reshape(-1, 2))
-                     for i in range(args.frames)]
+        unit_end = WAVE_WORDS + (2 << 22)
+        out[name] = []
+        for i in range(args.frames):
+            sm = summarise(raw[i, :WAVE_WORDS].reshape(-1, 4), raw[i, WAVE_WORDS:unit_end].reshape(-1, 2))
+            ph = raw[i, unit_end:].reshape(-1, 2).sum(0).astype(float)
+            sm["phase_ticks_share"] = {"primary": round(ph[0] / max(ph.sum(), 1), 3),
+                                       "shadow": round(ph[1] / max(ph.sum(), 1), 3)}
+            out[name].append(sm)
         print(name, json.dumps(out[name][-1]), flush=True)
     os.unlink(path)
     r.close()
