@@ -682,8 +682,10 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 
 __device__ __forceinline__ void flush_counters(const FrameArgs& a, uint32_t prim, uint32_t shadow,
                                                uint32_t nodes, uint32_t prims) {
-    const unsigned long long s0 = wave_sum(prim);
-    const unsigned long long s1 = wave_sum(shadow);
+    // ray counts are wave-uniform already (ballot counts); the work counters
+    // are per lane
+    const unsigned long long s0 = prim;
+    const unsigned long long s1 = shadow;
     const unsigned long long s2 = wave_sum(nodes);
     const unsigned long long s3 = wave_sum(prims);
     if ((threadIdx.x & 63u) == 0) {
@@ -742,15 +744,15 @@ __device__ __forceinline__ PixelOut sample_color(const FrameArgs& a, uint32_t x,
     const float s0 = p0 + n0 * kShadowEps, s1 = p1 + n1 * kShadowEps, s2 = p2 + n2 * kShadowEps;
     float ts;
     uint32_t is;
+    // ray counters are wave-uniform (SGPRs): lanes that cast, counted by ballot
+    n_shadow += static_cast<uint32_t>(__popcll(__ballot(want_shadow)));
     if (kVar == kVariantPacket) {
         if (__ballot(want_shadow)) {
-            n_shadow += want_shadow ? 1u : 0u;
             if (walk_packet<true>(S, want_shadow, s0, s1, s2, a.L[0], a.L[1], a.L[2], 0.0f, ts, is,
                                   n_nodes, n_prims, static_cast<PStackEntry*>(stk)))
                 lam = 0.0f;
         }
     } else if (want_shadow) {
-        n_shadow += 1;
         if (walk<true, kChunk>(S, s0, s1, s2, a.L[0], a.L[1], a.L[2], 0.0f, INFINITY, ts, is,
                                n_nodes, n_prims, static_cast<uint2*>(stk)))
             lam = 0.0f;
@@ -821,7 +823,7 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
             }
             active = want_shadow;
             any = true;
-            n_shadow += active ? 1u : 0u;
+            n_shadow += static_cast<uint32_t>(__popcll(__ballot(active)));  // wave-uniform
             if (!__any(active)) break;
         } else if (active && hit) {
             lam = 0.0f;
@@ -868,7 +870,7 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
     for (uint32_t r = 0; r < a.rounds; ++r) {
         const uint32_t sg = r * spw + sub_base;
         const bool valid = lane_ok && sg < s_end;
-        n_primary += valid ? 1u : 0u;
+        n_primary += static_cast<uint32_t>(__popcll(__ballot(valid)));  // wave-uniform
         PixelOut c = kVar == kVariantLaneUnified
                          ? sample_color_unified<kChunk, kStats, kLeafMode>(
                                a, x, y, hp, sg, valid, n_shadow, n_nodes, n_prims, stk, lbuf)
@@ -1051,7 +1053,7 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
     }
     flush_counters(a, n_primary, n_shadow, n_nodes, n_prims);
 #ifdef RT_TIMELINE
-    tl_units = n_primary;
+    tl_units = n_primary / 64u;  // samples cast by the wave / 64
     if (a.timeline && (threadIdx.x & 63u) == 0) {
         unsigned long long* e = a.timeline + 4ull * (blockIdx.x * (kBlockThreads / 64) + wave);
         e[0] = tl_start;
