@@ -1178,7 +1178,17 @@ static void launch_waveq(K kernel, const FrameArgs& a, size_t lds, hipStream_t s
     // (the grid only sizes the launch; padding units of edge blocks are skipped)
     const uint64_t want = (units + kBlockThreads / 64 - 1) / (kBlockThreads / 64);
     const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(res, want)));
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlockThreads), lds, st, a);
+    FrameArgs b = a;
+    if (!((a.sc.opt >> kOptChunkShift) & 7u)) {
+        // auto ticket size, second half: a small launch (a multi-GPU share)
+        // has few units per wave, and big tickets lengthen its tail. N-way
+        // C3 shares: 4 per ticket best at 1/2 and 1/4, 2 at 1/8 (36 units a
+        // wave; profiles/r01/shard_chunk.log)
+        const uint64_t per_wave = units / (static_cast<uint64_t>(grid) * (kBlockThreads / 64));
+        const uint32_t cap = per_wave >= 64 ? 4u : per_wave >= 16 ? 2u : 1u;
+        b.wq_chunk = std::min(b.wq_chunk, cap);
+    }
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlockThreads), lds, st, b);
 }
 
 template <bool kTiles>
