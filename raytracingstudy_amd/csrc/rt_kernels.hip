@@ -1194,12 +1194,12 @@ static void launch_waveq(K kernel, const FrameArgs& a, size_t lds, hipStream_t s
 template <bool kTiles>
 static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStream_t st) {
     if (a.accum) {  // progressive frames: the unified walk, whatever the A/B variant
-        if (a.spp >= 8u) {
+        if (a.spp >= 8u) {  // 7 waves/SIMD like variant 13 (no spills since the uniform counters)
             if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, true, true>,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, true, true, true>,
                              a, lds, st);
             else
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true, true>,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, false, true, true>,
                              a, lds, st);
         } else if (a.count_work) {
             launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, true>, a,
