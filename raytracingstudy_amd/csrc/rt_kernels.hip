@@ -1139,6 +1139,8 @@ static uint32_t resident_blocks(K kernel, size_t lds) {
     return n;
 }
 
+constexpr size_t kOneSppLds = (160u * 1024u / 3u) & ~size_t(15);  // 3 workgroups per CU
+
 // Block tiles in the frame (or in the packed tile list) for block-tile side b.
 static uint32_t count_block_tiles(const FrameArgs& a, uint32_t b) {
     if (a.tiles) return a.n_tiles * (a.tile_size / b) * (a.tile_size / b);
@@ -1154,6 +1156,11 @@ template <typename K>
 static void launch_persistent(K kernel, const FrameArgs& a_in, uint32_t, size_t lds,
                               hipStream_t st) {
     FrameArgs a = a_in;
+    // 1 spp: a wave's 64 lanes are 64 different pixels, whose walks thrash
+    // the L1 when 5 workgroups share a CU; the dynamic LDS is padded so that
+    // at most 3 are resident (C2: 0.358 -> 0.274 ms; 2 or 4 per CU slower,
+    // 4 spp unchanged; profiles/r01/c2_wg_cap_ab.log)
+    if (a.spw == 1u && !(a.sc.opt & kOptNoWgCap)) lds = std::max(lds, kOneSppLds);
     const uint32_t res = resident_blocks(kernel, lds);
     const uint32_t min_side = 2u * std::max(a.tw, a.th);
     a.bts = kTileSide;

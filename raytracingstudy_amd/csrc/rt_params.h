@@ -33,6 +33,7 @@ constexpr uint32_t kPrimPad = 4;           // prim_sp padding: scalar reads may 
 // A/B toggles (rt_config.flags bits 20..23), results identical either way
 constexpr uint32_t kOptBtsShift = 1;       // bits 1..3: force the block-tile side (A/B):
                                            // 0 auto, 1 = 16, 2 = 8, 3 = 4, 4 = 2 pixels
+constexpr uint32_t kOptNoWgCap = 1u << 7; // bit 7: 1-spp frames without the 3-workgroups-per-CU cap
 constexpr uint32_t kOptChunkShift = 4;     // bits 4..6: wave-queue tiles per ticket: 0 auto
                                            // (4 / rounds, at least 1), k = 1..4 -> 1 << (k - 1)
 
