@@ -238,8 +238,9 @@ def main():
             events.append((e0, e1))
         if tiled and not args.shard:
             gathered = sharder.gather(packed)  # RCCL gather of the equal-size slabs to rank 0
-            sharder.unpack(gathered, lambda slab, ids: r.unpack_tiles(slab.data_ptr(), ids, ts,
-                                                                      frame.data_ptr(), sptr))
+            # one unpack launch over all ranks' slabs (padding slots skipped)
+            sharder.unpack_fused(gathered, lambda buf, ids: r.unpack_tiles(buf.data_ptr(), ids, ts,
+                                                                          frame.data_ptr(), sptr))
 
     # counted rays of one frame on this rank (deterministic; equal to the oracle's)
     if not tiled:

@@ -229,7 +229,10 @@ int rt_bind_graphics_resource(rt_renderer* r, void* hip_graphics_resource);
  * pixels outside the image are written as 0.  Used to shard a frame over GPUs. */
 int rt_render_tiles(rt_renderer* r, const uint32_t* tile_ids, uint32_t n_tiles,
                     uint32_t tile_size, void* dev_packed_rgba8, void* stream, rt_stats* stats);
-/* Scatter a packed tile buffer (layout above) into a W*H*4 device image. */
+/* Scatter a packed tile buffer (layout above) into a W*H*4 device image.
+ * A tile id of RT_TILE_SKIP marks a padding slot that is not copied, so the
+ * equal-size slabs of all ranks, gathered into one buffer, unpack in one call. */
+#define RT_TILE_SKIP 0xFFFFFFFFu
 int rt_unpack_tiles(rt_renderer* r, const void* dev_packed_rgba8, const uint32_t* tile_ids,
                     uint32_t n_tiles, uint32_t tile_size, void* dev_rgba8, void* stream);
 /* RT_FLAG_PROGRESSIVE: start the next frame from zero samples (any change of

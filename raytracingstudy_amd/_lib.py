@@ -33,6 +33,7 @@ RT_FLAG_HOST_BUILD = 1 << 4
 RT_FLAG_PROGRESSIVE = 1 << 5
 RT_BUILDER_DEVICE = 0
 RT_BUILDER_HOST = 1
+RT_TILE_SKIP = 0xFFFFFFFF  # rt_unpack_tiles: a padding slot, not copied
 RT_FLAG_VARIANT_SHIFT = 16
 RT_FLAG_OPT_SHIFT = 20
 RT_FLAG_CELL_TABLE_SHIFT = 28

@@ -291,12 +291,14 @@ int check_octree_params(rt_renderer* r, const rt_octree_params* oct, const char*
     return RT_OK;
 }
 
-int check_tiles(rt_renderer* r, const uint32_t* ids, uint32_t n_tiles, uint32_t ts) {
+int check_tiles(rt_renderer* r, const uint32_t* ids, uint32_t n_tiles, uint32_t ts,
+                bool allow_skip = false) {
     if (ts == 0 || ts % 64 != 0 || ts > 4096)
         return fail(r, RT_E_INVALID, "tile_size must be a multiple of 64 in [64, 4096]");
     const uint32_t tx = (r->W + ts - 1) / ts, ty = (r->H + ts - 1) / ts;
     for (uint32_t i = 0; i < n_tiles; ++i)
-        if (ids[i] >= tx * ty) return fail(r, RT_E_INVALID, "tile id out of range");
+        if (ids[i] >= tx * ty && !(allow_skip && ids[i] == RT_TILE_SKIP))
+            return fail(r, RT_E_INVALID, "tile id out of range");
     return RT_OK;
 }
 
@@ -790,7 +792,7 @@ int rt_unpack_tiles(rt_renderer* r, const void* dev_packed, const uint32_t* tile
     if (!r) return fail(r, RT_E_INVALID, "rt_unpack_tiles: null handle");
     if (n_tiles && (!tile_ids || !dev_packed)) return fail(r, RT_E_INVALID, "rt_unpack_tiles: null argument");
     int st;
-    if ((st = check_tiles(r, tile_ids, n_tiles, ts))) return st;
+    if ((st = check_tiles(r, tile_ids, n_tiles, ts, /*allow_skip=*/true))) return st;
     if (n_tiles == 0) return RT_OK;
     const uint32_t tx = (r->W + ts - 1) / ts;
     if ((st = set_device(r))) return st;

@@ -1074,6 +1074,7 @@ __global__ void __launch_bounds__(kBlockThreads)
     const uint32_t k = static_cast<uint32_t>(i / per);
     const uint32_t r = static_cast<uint32_t>(i % per);
     const uint32_t tile = tiles[k];
+    if (tile == 0xFFFFFFFFu) return;  // RT_TILE_SKIP: a padding slot
     const uint32_t x = (tile % tiles_x) * ts + r % ts;
     const uint32_t y = (tile / tiles_x) * ts + r / ts;
     if (x < W && y < H) img[(size_t)y * W + x] = packed[i];

@@ -33,6 +33,11 @@ class TileSharder:
         self.ids = self.all_ids[self.rank]
         self.slab_tiles = T.slab_tiles(width, height, world, tile_size)
         self.slab_elems = self.slab_tiles * self.ts * self.ts * channels
+        # every rank's ids padded to the slab size with RT_TILE_SKIP: the
+        # gathered slabs, end to end in one buffer, unpack in ONE call
+        self.all_ids_padded = np.full(self.world * self.slab_tiles, T.TILE_SKIP, np.uint32)
+        for k, ids in enumerate(self.all_ids):
+            self.all_ids_padded[k * self.slab_tiles:k * self.slab_tiles + len(ids)] = ids
 
     def new_slab(self, torch_mod, device=None, dtype=None):
         """Zeroed packed slab for this rank (uint8 RGBA by default)."""
@@ -54,13 +59,28 @@ class TileSharder:
         if self.rank == 0:
             key = (tuple(src.shape), src.dtype, src.device)
             if getattr(self, "_recv_key", None) != key:
-                self._recv = [torch.empty_like(src) for _ in range(self.world)]
+                # the receive slabs are views of ONE buffer (unpack_fused)
+                self._recv_buf = torch.empty((self.world,) + tuple(src.shape), dtype=src.dtype,
+                                             device=src.device)
+                self._recv = list(self._recv_buf.unbind(0))
                 self._recv_key = key
             out = self._recv
         dist.gather(src, out, dst=0, group=group)
         if staged and out is not None:
             out = [t.to(slab.device) for t in out]
         return out
+
+    def unpack_fused(self, gathered, unpack_fn: Callable[[object, np.ndarray], None]) -> None:
+        """Rank 0: ONE unpack_fn(buffer, all_ids_padded) call over every rank's
+        slab, end to end in one contiguous buffer (padding slots are
+        RT_TILE_SKIP), instead of one call per rank."""
+        if self.rank != 0:
+            return
+        import torch
+        buf = getattr(self, "_recv_buf", None)
+        if buf is None or gathered[0].data_ptr() != buf.data_ptr():
+            buf = torch.stack(list(gathered))  # staged (gloo) slabs: make them contiguous
+        unpack_fn(buf, self.all_ids_padded)
 
     def unpack(self, gathered, unpack_fn: Callable[[object, np.ndarray], None]) -> None:
         """Rank 0: call unpack_fn(slab_k, tile_ids_k) for every rank's slab."""

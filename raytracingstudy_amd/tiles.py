@@ -10,7 +10,9 @@ from __future__ import annotations
 
 import numpy as np
 
-__all__ = ["tile_grid", "tiles_for_rank", "slab_tiles", "pack_reference", "unpack_host"]
+__all__ = ["tile_grid", "tiles_for_rank", "slab_tiles", "pack_reference", "unpack_host", "TILE_SKIP"]
+
+TILE_SKIP = 0xFFFFFFFF  # include/rt.h RT_TILE_SKIP: a padding slot of a gathered slab
 
 
 def tile_grid(width: int, height: int, ts: int = 64):
@@ -75,6 +77,8 @@ def unpack_host(packed: np.ndarray, tile_ids, width: int, height: int, ts: int =
         out = np.zeros((height, width, packed.shape[-1]), packed.dtype)
     packed = packed.reshape(-1, ts, ts, packed.shape[-1])
     for k, t in enumerate(np.asarray(tile_ids, np.int64)):
+        if t == TILE_SKIP:
+            continue
         x0, y0 = (t % tx) * ts, (t // tx) * ts
         h, w = min(ts, height - y0), min(ts, width - x0)
         out[y0:y0 + h, x0:x0 + w] = packed[k, :h, :w]

@@ -413,3 +413,32 @@ def test_wave_queue_ticket_sizes(gpu, oracle, n, w, h, spp, chunk_bits):
     ref8, ref32, cnt = oracle.Scene(sp, al).render(w, h, scene_pose(), K, spp=spp)
     assert np.array_equal(img, ref8) and np.array_equal(rad, ref32)
     _check_counts(st, cnt, 0)
+
+
+def test_fused_unpack_with_padding_slots(gpu):
+    """The bench's rank-0 path: every rank's equal-size slab end to end in one
+    buffer, unpacked by ONE rt_unpack_tiles call whose padding slots are
+    RT_TILE_SKIP (TileSharder.unpack_fused); render_tiles still rejects it."""
+    import torch
+    from raytracingstudy_amd.dist import TileSharder
+    w, h, ts, world = 300, 200, 64, 3  # 20 tiles: slabs of 7, the last rank pads one
+    sp, al = rt.generate_spheres(5000, rt.SEED)
+    with rt.KernelRenderer(w, h, mode="scene", spp=4) as r:
+        r.resize(w, h)
+        r.setPosition(scene_pose())
+        r.set_scene(sp, al)
+        r.render()
+        full = r.readback()
+        shards = [TileSharder(w, h, k, world, ts) for k in range(world)]
+        n = shards[0].slab_tiles
+        assert any(len(s.ids) < n for s in shards)
+        buf = torch.zeros(world * n * ts * ts * 4, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        for k, s in enumerate(shards):
+            r.render_tiles(s.ids, ts, buf.data_ptr() + k * n * ts * ts * 4)
+        img = torch.zeros(w * h * 4, dtype=torch.uint8, device="cuda")
+        r.unpack_tiles(buf.data_ptr(), shards[0].all_ids_padded, ts, img.data_ptr())
+        r.synchronize()
+        assert np.array_equal(img.cpu().numpy().reshape(h, w, 4), full)
+        with pytest.raises(RuntimeError):
+            r.render_tiles(np.array([rt._lib.RT_TILE_SKIP], np.uint32), ts, buf.data_ptr())

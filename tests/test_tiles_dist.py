@@ -83,17 +83,24 @@ def _rank_main(rank, world, port, w, h, spp, q):
         view[k, :blk.shape[0], :blk.shape[1]] = blk
     gathered = sh.gather(slab)
     if rank == 0:
-        q.put(sh.unpack_host(gathered))
+        per_rank = sh.unpack_host(gathered)
+        # the bench's fused unpack: all slabs end to end, padding slots skipped
+        fused = {}
+        sh.unpack_fused(gathered, lambda buf, ids: fused.setdefault(
+            "img", T.unpack_host(buf.numpy().reshape(-1, 64, 64, 4), ids, w, h)))
+        assert np.array_equal(fused["img"], per_rank)
+        q.put(per_rank)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gloo_world2_gather_reproduces_frame(oracle):
+@pytest.mark.parametrize("world", [2, 5])  # 12 tiles: 5 ranks leave padding slots
+def test_gloo_world2_gather_reproduces_frame(oracle, world):
     import torch.multiprocessing as mp
     from raytracingstudy_amd.configs import SEED
     from raytracingstudy_amd.camera import scene_pose
 
-    w, h, spp, world = 200, 130, 2, 2
+    w, h, spp = 200, 130, 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
