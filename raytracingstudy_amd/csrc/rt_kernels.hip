@@ -300,13 +300,15 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             }
         }
         const float4* __restrict__ ps = prim_sp + off;
-        const uint32_t last = cnt - 1;
+        static_assert(kChunk <= kPrimPad + 1, "leaf loads may run kChunk-1 spheres past a leaf");
         for (uint32_t j = 0; j < cnt; j += kChunk) {
             const uint32_t m = cnt - j;
-            // unconditional loads clamped to the leaf: kChunk dwordx4 in flight
+            // kChunk unconditional dwordx4 loads in flight at fixed offsets; a
+            // slot past the leaf's end reads the next leaf or the array's
+            // kPrimPad tail (in bounds) and is never tested
             float4 sv[kChunk];
 #pragma unroll
-            for (int q = 0; q < kChunk; ++q) sv[q] = ps[min(j + q, last)];
+            for (int q = 0; q < kChunk; ++q) sv[q] = ps[j + q];
 #pragma unroll
             for (int q = 0; q < kChunk; ++q)
                 if (m > static_cast<uint32_t>(q) && test(sv[q], off + j + q)) return true;
