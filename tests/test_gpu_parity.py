@@ -442,3 +442,49 @@ def test_fused_unpack_with_padding_slots(gpu):
         assert np.array_equal(img.cpu().numpy().reshape(h, w, 4), full)
         with pytest.raises(RuntimeError):
             r.render_tiles(np.array([rt._lib.RT_TILE_SKIP], np.uint32), ts, buf.data_ptr())
+
+
+def _fuzz_case(seed: int):
+    """One seeded random scene / camera / render setting (test_scene_fuzz)."""
+    g = np.random.default_rng(seed)
+    n = int(g.choice([0, 1, 7, 50, 400, 3000]))
+    ctr = g.uniform(-0.2, 1.48, (n, 3))
+    rad = g.uniform(0.002, 0.25, n) * g.choice([1.0, 0.1], n)
+    sp = np.concatenate([ctr, rad[:, None]], 1).astype(np.float32)
+    al = g.integers(0, 1 << 24, n, dtype=np.uint32) | np.uint32(0xFF000000)
+    depth = int(g.integers(1, 13))
+    leaf = int(g.integers(1, 17))
+    spp = int(g.choice([1, 2, 3, 8, 64, 65]))
+    w, h = int(g.integers(1, 70)), int(g.integers(1, 50))
+    pos = g.uniform(-1.0, 2.3, 3)
+    pose = display_pose(tuple(pos), float(g.uniform(-180, 180)), float(g.uniform(-80, 80)))
+    light = tuple(float(x) for x in g.normal(size=3))
+    return dict(n=n, sp=sp, al=al, depth=depth, leaf=leaf, spp=spp, w=w, h=h, pose=pose,
+                light=light, ambient=float(g.uniform(0.0, 0.5)), shadows=bool(g.integers(0, 2)),
+                jitter=bool(g.integers(0, 2)) if spp > 1 else None)
+
+
+@pytest.mark.parametrize("seed", range(64))
+def test_scene_fuzz(gpu, oracle, seed):
+    """Seeded random scenes (spheres inside, across and outside the box, big
+    and tiny), depths 1..12, leaf capacities 1..16, spp 1..65, random poses
+    (inside the box too), light directions, ambient, shadows and jitter on or
+    off, odd frame sizes: RGBA8, radiance and the four counters equal the
+    oracle's."""
+    c = _fuzz_case(seed)
+    with rt.KernelRenderer(c["w"], c["h"], mode="scene", spp=c["spp"], radiance=True,
+                           shadows=c["shadows"], jitter=c["jitter"], light_dir=c["light"],
+                           ambient=c["ambient"]) as r:
+        r.resize(c["w"], c["h"])
+        r.setPosition(c["pose"])
+        r.set_scene(c["sp"], c["al"], max_depth=c["depth"], leaf_capacity=c["leaf"])
+        st = r.render(stats=True)
+        img, rad = r.readback(), r.readback_radiance()
+        _, K = r.camera()
+    ref8, ref32, cnt = oracle.Scene(c["sp"], c["al"], max_depth=c["depth"],
+                                    leaf_capacity=c["leaf"]).render(
+        c["w"], c["h"], c["pose"], K, spp=c["spp"], jitter=c["jitter"], shadows=c["shadows"],
+        light_dir=c["light"], ambient=c["ambient"])
+    assert np.array_equal(img, ref8)
+    assert np.array_equal(rad, ref32)
+    _check_counts(st, cnt, 0)
