@@ -16,6 +16,7 @@
 #include "oracle.h"
 
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -199,11 +200,24 @@ struct orc_scene {
     float G;
 };
 
-static uint32_t new_node(orc_scene* s) {
-    if (s->n_nodes == s->cap_nodes) {
-        s->cap_nodes = s->cap_nodes ? 2 * s->cap_nodes : 1024;
-        s->nodes = (onode*)realloc(s->nodes, sizeof(onode) * s->cap_nodes);
+/* The oracle is test infrastructure: a scene whose tree outgrows 32-bit
+ * counts or host memory stops the process with a message instead of
+ * corrupting memory (the product's builders report such scenes as errors). */
+static void* grow(void* p, uint32_t* cap, uint32_t first, size_t elem, const char* what) {
+    const uint64_t next = *cap ? 2ull * *cap : first;
+    void* q = next < (1ull << 31) ? realloc(p, elem * (size_t)next) : NULL;
+    if (!q) {
+        fprintf(stderr, "oracle: octree %s exceed %llu entries or host memory\n", what,
+                (unsigned long long)next);
+        abort();
     }
+    *cap = (uint32_t)next;
+    return q;
+}
+
+static uint32_t new_node(orc_scene* s) {
+    if (s->n_nodes == s->cap_nodes)
+        s->nodes = (onode*)grow(s->nodes, &s->cap_nodes, 1024, sizeof(onode), "nodes");
     onode* nd = &s->nodes[s->n_nodes];
     for (int i = 0; i < 8; ++i) nd->child[i] = -1;
     nd->leaf = 0;
@@ -212,10 +226,8 @@ static uint32_t new_node(orc_scene* s) {
 }
 
 static void push_prim(orc_scene* s, uint32_t idx) {
-    if (s->n_prims == s->cap_prims) {
-        s->cap_prims = s->cap_prims ? 2 * s->cap_prims : 4096;
-        s->prims = (uint32_t*)realloc(s->prims, sizeof(uint32_t) * s->cap_prims);
-    }
+    if (s->n_prims == s->cap_prims)
+        s->prims = (uint32_t*)grow(s->prims, &s->cap_prims, 4096, sizeof(uint32_t), "references");
     s->prims[s->n_prims++] = idx;
 }
 

@@ -437,7 +437,10 @@ hipError_t GpuOctreeBuilder::build(const float4* sp, uint32_t n, const float cfg
     int cur = 0;
     for (uint32_t depth = 0; M > 0; ++depth) {
         g.depth = depth;
-        if (uint64_t(R) * 8u + 1u >= (uint64_t(1) << 32)) return hipErrorInvalidValue;
+        if (uint64_t(R) * 8u + 1u >= (uint64_t(1) << 32)) {  // 8 flag slots per reference
+            res->ref_overflow = R;
+            return hipErrorInvalidValue;
+        }
         const uint32_t nf = 8u * R + 1u;
         RT_TRY(reserve(flags_, nf, 0, st));
         RT_TRY(reserve(pos_, nf, 0, st));

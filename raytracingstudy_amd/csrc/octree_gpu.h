@@ -14,6 +14,7 @@ namespace rtamd {
 struct GpuBuildResult {
     uint32_t n_nodes = 0, n_prims = 0, n_leaves = 0, depth_reached = 0;
     uint32_t n_invalid = 0;  // spheres with r <= 0 or a non-finite value (build refused)
+    uint64_t ref_overflow = 0;  // references of the level that exceeded the 32-bit slots (refused)
     float rmin[3] = {0, 0, 0}, rmax[3] = {0, 0, 0};
     uint2 root = {0, 0};
     bool root_is_leaf = true;

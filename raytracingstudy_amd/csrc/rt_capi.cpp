@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -205,7 +206,11 @@ int build_scene(rt_renderer* r) {
             r->host_copy = true;
         }
         BuiltOctree tree;
-        build_octree(r->spheres.data(), n, p.min, p.max, depth, cap, tree);
+        try {
+            build_octree(r->spheres.data(), n, p.min, p.max, depth, cap, tree);
+        } catch (const std::exception& ex) {  // bad_alloc / length_error: never through the C-ABI
+            return fail(r, RT_E_NOMEM, std::string("host octree build: ") + ex.what());
+        }
         const size_t nn = tree.nodes.size(), np = tree.prim_idx.size();
         if ((st = ensure(r, r->d_nodes, nn))) return st;
         if ((st = ensure(r, r->d_prim_sp, np + kPrimPad))) return st;  // scalar-read padding
@@ -233,6 +238,11 @@ int build_scene(rt_renderer* r) {
     } else {
         GpuBuildResult res;
         hipError_t e = r->gpu_build.build(r->d_spheres.p, n, p.min, p.max, depth, cap, r->stream, &res);
+        if (res.ref_overflow)
+            return fail(r, RT_E_INVALID,
+                        "scene too large for the octree: " + std::to_string(res.ref_overflow) +
+                            " sphere references in one level (limit 2^29); lower max_depth or "
+                            "raise leaf_capacity");
         if (e != hipSuccess) return hip_fail(r, e, "device octree build");
         if (res.n_invalid)
             return fail(r, RT_E_INVALID, "scene has spheres with radius <= 0 or non-finite values");

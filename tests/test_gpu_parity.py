@@ -448,12 +448,14 @@ def _fuzz_case(seed: int):
     """One seeded random scene / camera / render setting (test_scene_fuzz)."""
     g = np.random.default_rng(seed)
     n = int(g.choice([0, 1, 7, 50, 400, 3000]))
-    ctr = g.uniform(-0.2, 1.48, (n, 3))
-    rad = g.uniform(0.002, 0.25, n) * g.choice([1.0, 0.1], n)
-    sp = np.concatenate([ctr, rad[:, None]], 1).astype(np.float32)
-    al = g.integers(0, 1 << 24, n, dtype=np.uint32) | np.uint32(0xFF000000)
     depth = int(g.integers(1, 13))
     leaf = int(g.integers(1, 17))
+    # big spheres only in shallow trees: thousands of overlapping 0.25-radius
+    # spheres at depth 10 need ~10^8 cells (test_device_build_refuses_...)
+    ctr = g.uniform(-0.2, 1.48, (n, 3))
+    rad = g.uniform(0.002, 0.25 if depth <= 5 else 0.04, n) * g.choice([1.0, 0.1], n)
+    sp = np.concatenate([ctr, rad[:, None]], 1).astype(np.float32)
+    al = g.integers(0, 1 << 24, n, dtype=np.uint32) | np.uint32(0xFF000000)
     spp = int(g.choice([1, 2, 3, 8, 64, 65]))
     w, h = int(g.integers(1, 70)), int(g.integers(1, 50))
     pos = g.uniform(-1.0, 2.3, 3)
@@ -488,3 +490,23 @@ def test_scene_fuzz(gpu, oracle, seed):
     assert np.array_equal(img, ref8)
     assert np.array_equal(rad, ref32)
     _check_counts(st, cnt, 0)
+
+
+def test_device_build_refuses_oversize_tree(gpu):
+    """3,000 spheres of radius up to 0.25 at depth 10 with leaf capacity 4 need
+    ~10^8 cells: the device builder refuses with a clear error (no crash, no
+    silent truncation) instead of overflowing its 32-bit reference slots."""
+    g = np.random.default_rng(45)
+    n = 3000
+    sp = np.concatenate([g.uniform(-0.2, 1.48, (n, 3)), g.uniform(0.002, 0.25, (n, 1))],
+                        1).astype(np.float32)
+    with rt.KernelRenderer(16, 16, mode="scene", spp=1) as r:
+        with pytest.raises(rt._lib.RtError) as ei:
+            r.set_scene(sp, max_depth=10, leaf_capacity=4)
+        assert ei.value.code in (rt._lib.RT_E_INVALID, rt._lib.RT_E_NOMEM)
+        if ei.value.code == rt._lib.RT_E_INVALID:
+            assert "too large" in str(ei.value)
+        # the renderer stays usable with a sane scene
+        sp2, al2 = rt.generate_spheres(100, rt.SEED)
+        r.set_scene(sp2, al2)
+        r.render()
