@@ -308,7 +308,12 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             // kPrimPad tail (in bounds) and is never tested
             float4 sv[kChunk];
 #pragma unroll
-            for (int q = 0; q < kChunk; ++q) sv[q] = ps[j + q];
+            for (int q = 0; q < kChunk; ++q) {
+                sv[q] = ps[j + q];
+                // issue in list order, so the first test waits for its own
+                // sphere only (vmcnt(kChunk-1)), not for the whole chunk
+                __builtin_amdgcn_sched_barrier(0);
+            }
 #pragma unroll
             for (int q = 0; q < kChunk; ++q)
                 if (m > static_cast<uint32_t>(q) && test(sv[q], off + j + q)) return true;
