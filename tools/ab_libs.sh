@@ -1,11 +1,18 @@
 #!/usr/bin/env bash
-# A/B of several build_ab/librt_<name>.so builds, interleaved (c3, c5)
+# A/B of several builds (build_ab/librt_<name>.so from tools/build_rev.sh, or
+# copies of the in-tree library), interleaved per repetition so drift hits all
+# of them alike.  Run on the GPU box from the repo root (build_ab must not be
+# in .gpurunignore for that call).
+# usage: bash tools/ab_libs.sh <log> <configs> <reps> <name>...
+#   e.g. bash tools/ab_libs.sh gpurun_out/leaf_chunk_ab.log c3,c5 3 base ck3 ck4
 set -e -o pipefail
+LOG=${1:?log}; CFGS=${2:?configs}; REPS=${3:?reps}; shift 3
+[ $# -ge 1 ] || { echo "name at least one build" >&2; exit 2; }
 export TMPDIR=/tmp
-LOG=gpurun_out/leaf_chunk_ab.log
-mkdir -p gpurun_out
-for i in 1 2 3; do
-  for L in base ck3 ck4; do
-    RT_AMD_LIB=build_ab/librt_$L.so timeout -k 10 200 python tools/variants.py --configs c3,c5 --variants 0 --rounds 5 | sed "s/^/$L /" >> $LOG
+mkdir -p "$(dirname "$LOG")"
+for i in $(seq "$REPS"); do
+  for L in "$@"; do
+    RT_AMD_LIB=build_ab/librt_$L.so timeout -k 10 200 python tools/variants.py --configs "$CFGS" \
+        --variants 0 --rounds 5 | sed "s/^/$L /" >> "$LOG"
   done
 done
