@@ -99,34 +99,74 @@ def cpu_baseline(cfg, K, pose, target_s: float) -> dict:
                             "sample": f"every {s1}th row ({rays1} rays) in {el1:.2f} s"}}
 
 
-def pmc_figures(path: str, cfg_name: str, world: int, kern_ms: float, simds: int):
-    """(HBM bytes per launch, VALU-issue roofline dict) from the committed PMC
-    summary (tools/pmc_traffic.py output: one flat object naming its config),
-    or (None, None) when it is missing or was taken on another config."""
+def load_pmc(path: str, cfg_name: str, world: int, src_id: str):
+    """The committed PMC summary (tools/pmc_traffic.py output) for this config
+    and GPU count, or (None, reason) when it is missing, taken on another
+    config, or stamped with other kernel sources than this build's."""
     try:
         with open(path) as f:
             pm = json.load(f)
-    except (OSError, ValueError):
-        return None, None
+    except (OSError, ValueError) as e:
+        return None, f"no PMC summary ({e.__class__.__name__})"
     ent = pm if pm.get("config") == cfg_name else pm.get(cfg_name)
     if not isinstance(ent, dict) or ent.get("n_gpus", 1) != world:
-        return None, None
-    traffic = ent.get("hbm_bytes_per_launch")
-    insts = ent.get("valu_insts_per_launch", ent.get("sq", {}).get("SQ_INSTS_VALU"))
-    clock = ent.get("clock_ghz", ent.get("effective_clock_ghz"))
-    if not (insts and clock):
-        return traffic, None
-    # what bounds this kernel: VALU issue (a wave64 VALU instruction occupies a
-    # SIMD-32 for 2 cycles, MI355X_MICROARCH.md), with the PMC instruction count
-    # over the live kernel time
-    peak = simds * clock * 1e9 / 2.0
-    rate = insts / (kern_ms / 1e3)
-    valu = {"insts_per_launch": insts, "achieved_winst_per_s": round(rate / 1e9, 2),
-            "peak_winst_per_s": round(peak / 1e9, 2), "unit": "G wave-instr/s",
-            "frac": round(rate / peak, 4), "clock_ghz": round(clock, 4),
-            "source": "rocprofv3 --pmc SQ_INSTS_VALU, GRBM_GUI_ACTIVE "
-                      f"({os.path.relpath(path, ROOT)})"}
-    return traffic, valu
+        return None, f"PMC summary is not for {cfg_name} on {world} GPU(s)"
+    if ent.get("kernel_source_id") != src_id:
+        return None, (f"PMC summary stamped {ent.get('kernel_source_id')!r}, kernel sources are "
+                      f"{src_id!r}: stale, not used")
+    return ent, "ok"
+
+
+def roofline(kern_ms: float, touched_bytes: float, pmc, simds: int, pmc_path: str = "",
+             pmc_note: str = "") -> dict:
+    """Every roof this kernel could sit under, each computed from measured data,
+    and the binding one (largest valid fraction) on top:
+      * valu_issue: PMC SQ_INSTS_VALU per launch over the live kernel time,
+        against SIMDs x clock / 2 (a wave64 VALU instruction occupies a
+        SIMD-32 for 2 cycles, MI355X_MICROARCH.md "Wave scheduling");
+      * hbm: PMC HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950
+        correction) over the live kernel time, against 8 TB/s;
+      * l2: SURVEY 8d D4 algorithmic bytes (node + sphere records touched per
+        ray) against the L2s' aggregate bandwidth.  Those bytes are served by
+        L1/L2 (the scene is cache-resident), never by HBM, so they are never
+        priced against HBM.
+    A fraction > 1 is not a valid roof and is never chosen."""
+    secs = kern_ms / 1e3
+    roofs = {}
+    traffic = None
+    if pmc:
+        traffic = pmc.get("hbm_bytes_per_launch")
+        insts = pmc.get("valu_insts_per_launch", pmc.get("sq", {}).get("SQ_INSTS_VALU"))
+        clock = pmc.get("clock_ghz", pmc.get("effective_clock_ghz"))
+        src = f"rocprofv3 --pmc ({os.path.relpath(pmc_path, ROOT) if pmc_path else 'PMC summary'}, " \
+              f"kernel sources {pmc.get('kernel_source_id')})"
+        if insts and clock:
+            peak = simds * clock * 1e9 / 2.0
+            rate = insts / secs
+            roofs["valu_issue"] = {"achieved": round(rate / 1e9, 2), "peak": round(peak / 1e9, 2),
+                                   "unit": "G wave-instr/s", "frac": round(rate / peak, 4),
+                                   "insts_per_launch": insts, "clock_ghz": round(clock, 4),
+                                   "simds": simds, "source": src + ": SQ_INSTS_VALU, GRBM_GUI_ACTIVE"}
+        if traffic:
+            rate = traffic / secs / 1e9
+            roofs["hbm"] = {"achieved": round(rate, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(rate / HBM_PEAK_GBS, 6), "bytes_per_launch": traffic,
+                            "source": src + ": 2 x FETCH_SIZE + WRITE_SIZE"}
+    l2 = touched_bytes / secs / 1e9
+    roofs["l2"] = {"achieved": round(l2, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",
+                   "frac": round(l2 / L2_PEAK_GBS, 4), "touched_bytes_per_launch": int(touched_bytes),
+                   "source": "SURVEY 8d D4 algorithmic bytes (oracle counters) vs "
+                             "MI355X_MICROARCH.md L2 aggregate ~34.5 TB/s; L1/L2-served"}
+    valid = {k: v for k, v in roofs.items() if v["frac"] <= 1.0}
+    bound = max(valid, key=lambda k: valid[k]["frac"]) if valid else None
+    top = roofs[bound] if bound else {}
+    out = {"bound": bound, "achieved": top.get("achieved"), "peak": top.get("peak"),
+           "unit": top.get("unit"), "frac": top.get("frac"), "traffic": traffic,
+           "touched_bytes": int(touched_bytes),
+           "roofs": roofs}
+    if not pmc:
+        out["pmc"] = pmc_note
+    return out
 
 
 def secondary_config(rt, torch, name: str, dev, stream, steps: int = 3) -> dict:
@@ -280,9 +320,11 @@ def main():
         # roofline of the dominant kernel on this rank: algorithmic bytes per launch
         pix = (W * H) if not tiled else len(my_ids) * ts * ts
         alg_bytes = float(cnt[2].item()) * NODE_BYTES + float(cnt[3].item()) * PRIM_BYTES + pix * PIXEL_BYTES
-        achieved = alg_bytes / (kern_ms / 1e3) / 1e9
         simds = torch.cuda.get_device_properties(dev).multi_processor_count * 4
-        traffic, valu = pmc_figures(args.pmc, cfg.name, world, kern_ms, simds)
+        pmc, pmc_note = load_pmc(args.pmc, cfg.name, world, rt._lib.kernel_source_id())
+        roof = roofline(kern_ms, alg_bytes, pmc if not tiled else None, simds, args.pmc, pmc_note)
+        roof["per_ray"] = {"nodes": float(cnt[2].item()) / float(cnt[0].item() + cnt[1].item()),
+                           "prims": float(cnt[3].item()) / float(cnt[0].item() + cnt[1].item())}
         out = {
             "metric": f"Mrays/s (primary+shadow) at {W}x{H}, {cfg.spp} spp, {cfg.n_spheres} spheres",
             "value": round(value, 3),
@@ -308,23 +350,7 @@ def main():
                 "scene_build_ms": round(info["build_ms"], 1),
                 "scene_upload_ms": round(info["upload_ms"], 1),
             },
-            "roofline": {
-                "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                "alg_bytes_per_launch": int(alg_bytes),
-                "note": ("algorithmic bytes = SURVEY 8d D4 node+sphere records touched per ray + "
-                         "framebuffer; the octree is cache-resident (L1/L2/MALL), so HBM sees only "
-                         "`traffic` bytes per launch (PMC, corrected)"),
-                "hbm_traffic_gbs": (round(traffic / (kern_ms / 1e3) / 1e9, 3) if traffic else None),
-                "per_ray": {"nodes": float(cnt[2].item()) / float(cnt[0].item() + cnt[1].item()),
-                            "prims": float(cnt[3].item()) / float(cnt[0].item() + cnt[1].item())},
-                "valu_issue": valu,
-                # where the touched bytes are actually served from: the same
-                # algorithmic bytes against the L2s' aggregate bandwidth
-                "l2": {"peak": L2_PEAK_GBS, "unit": "GB/s",
-                       "frac": round(achieved / L2_PEAK_GBS, 4),
-                       "source": "MI355X_MICROARCH.md L2 (per XCD): ~34.5 TB/s aggregate"},
-            },
+            "roofline": roof,
             "cpu_baseline": None,
         }
         if args.shard:

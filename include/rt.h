@@ -239,10 +239,14 @@ int rt_unpack_tiles(rt_renderer* r, const void* dev_packed_rgba8, const uint32_t
  * pose, intrinsic, size, scene or tile list does this by itself; setting the
  * same pose again, as the reference's Displayer does every frame, does not). */
 int rt_reset_accumulation(rt_renderer* r);
-/* Wait for all work queued by this renderer. */
+/* Wait for all work queued by this renderer, on its own stream or on the
+ * caller streams passed to rt_render / rt_render_tiles / rt_unpack_tiles.
+ * (Work queued on a stream other than the previous call's is ordered after
+ * that previous call's work: the renderer's counters and buffers are shared.) */
 int rt_synchronize(rt_renderer* r);
 /* Copy the internal framebuffer (and the float4 radiance buffer when
- * RT_FLAG_RADIANCE is set) to host memory; either pointer may be NULL. */
+ * RT_FLAG_RADIANCE is set) to host memory; either pointer may be NULL.
+ * Waits for the renderer's queued work first, whatever stream it is on. */
 int rt_readback(rt_renderer* r, uint8_t* host_rgba8, float* host_rgba32f);
 /* Device pointer of the internal framebuffer (W*H*4 bytes). */
 void* rt_framebuffer(rt_renderer* r);

@@ -149,6 +149,22 @@ SIGNATURES = {
 _lock = threading.Lock()
 _lib = None
 
+# the sources the scene kernel's machine code is built from (device code and
+# its compile flags): a PMC summary is valid for a build iff its stamp matches
+KERNEL_SOURCES = ("csrc/rt_kernels.hip", "csrc/rt_params.h", "csrc/Makefile")
+
+
+def kernel_source_id() -> str:
+    """sha256 (first 16 hex digits) of KERNEL_SOURCES: stamps profiles/ PMC
+    summaries (tools/pmc_traffic.py) so bench.py uses counters only for the
+    kernel they were collected on."""
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(_HERE, rel), "rb") as f:
+            h.update(rel.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
 
 class RtError(RuntimeError):
     def __init__(self, code: int, msg: str):

@@ -468,6 +468,14 @@ hipError_t GpuOctreeBuilder::build(const float4* sp, uint32_t n, const float cfg
         RT_TRY(hipMemcpyAsync(totals_host_, totals_.p, sizeof(uint4), hipMemcpyDeviceToHost, st));
         RT_TRY(hipStreamSynchronize(st));
         const uint4 t = *totals_host_;  // x next cells, y leaf refs, z leaves, w next refs
+        // node slots and leaf-list offsets are 32-bit record fields: refuse
+        // (the caller then builds on the host, which refuses the same way)
+        // rather than wrap
+        if (uint64_t(prim_total) + t.y + kPrimPad >= (uint64_t(1) << 32) ||
+            uint64_t(next_start) + t.x >= (uint64_t(1) << 32)) {
+            res->ref_overflow = uint64_t(prim_total) + t.y;
+            return hipErrorInvalidValue;
+        }
         const int nxt = cur ^ 1;
         RT_TRY(reserve(nodes_b_, size_t(next_start) + t.x, next_start, st));
         RT_TRY(reserve(prim_idx_b_, size_t(prim_total) + t.y + 1, prim_total, st));

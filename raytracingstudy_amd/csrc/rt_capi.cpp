@@ -24,6 +24,7 @@
 namespace rtamd {
 hipError_t launch_compat(const FrameArgs& a, hipStream_t st);
 hipError_t launch_scene(const FrameArgs& a, hipStream_t st);
+bool variant_available(uint32_t v);
 hipError_t launch_unpack(const uint32_t* packed, const uint32_t* tiles, uint32_t n_tiles,
                          uint32_t ts, uint32_t tiles_x, uint32_t W, uint32_t H, uint32_t* img,
                          hipStream_t st);
@@ -51,6 +52,13 @@ struct rt_renderer {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // completion of the renderer's last queued work (render, tiles, unpack) on
+    // whichever stream it ran: a launch on another stream is ordered after it
+    // (the counters, queue heads and buffers are shared), and
+    // rt_synchronize / rt_readback wait for it
+    hipEvent_t done = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool pending = false;
     float pose[16];
     float K[9];
     uint32_t W = 0, H = 0;
@@ -197,7 +205,36 @@ int build_scene(rt_renderer* r) {
     SceneArgs& sc = r->sc;
     float rmin[3], rmax[3];
     auto t0 = std::chrono::steady_clock::now();
-    if (r->cfg.flags & RT_FLAG_HOST_BUILD) {
+    bool host = (r->cfg.flags & RT_FLAG_HOST_BUILD) != 0;
+    if (!host) {
+        GpuBuildResult res;
+        hipError_t e = r->gpu_build.build(r->d_spheres.p, n, p.min, p.max, depth, cap, r->stream, &res);
+        if (res.n_invalid)
+            return fail(r, RT_E_INVALID, "scene has spheres with radius <= 0 or non-finite values");
+        if ((r->cfg.flags >> RT_FLAG_OPT_SHIFT) & kOptDeviceBuildRefuse) res.ref_overflow = 1;
+        if (res.ref_overflow || e == hipErrorOutOfMemory) {
+            // the device builder's 32-bit per-level slots (or HBM) cannot hold
+            // this tree: build the identical tree on the host instead
+            (void)hipGetLastError();
+            host = true;
+        } else if (e != hipSuccess) {
+            return hip_fail(r, e, "device octree build");
+        } else {
+            sc.nodes = r->gpu_build.nodes();
+            sc.prim_sp = r->gpu_build.prim_sp();
+            sc.prim_idx = r->gpu_build.prim_idx();
+            sc.root = res.root;
+            sc.root_is_leaf = res.root_is_leaf ? 1u : 0u;
+            in.n_nodes = res.n_nodes;
+            in.n_leaves = res.n_leaves;
+            in.n_prim_refs = res.n_prims;
+            in.depth_reached = res.depth_reached;
+            in.builder = RT_BUILDER_DEVICE;
+            memcpy(rmin, res.rmin, sizeof(rmin));
+            memcpy(rmax, res.rmax, sizeof(rmax));
+        }
+    }
+    if (host) {
         if (!r->host_copy) {
             r->spheres.resize(4u * n);
             if (n)
@@ -208,7 +245,10 @@ int build_scene(rt_renderer* r) {
         BuiltOctree tree;
         try {
             build_octree(r->spheres.data(), n, p.min, p.max, depth, cap, tree);
-        } catch (const std::exception& ex) {  // bad_alloc / length_error: never through the C-ABI
+        } catch (const std::length_error& ex) {  // past the 32-bit record fields
+            return fail(r, RT_E_INVALID, std::string("scene too large for the octree: ") + ex.what() +
+                                             "; lower max_depth or raise leaf_capacity");
+        } catch (const std::exception& ex) {  // bad_alloc: never through the C-ABI
             return fail(r, RT_E_NOMEM, std::string("host octree build: ") + ex.what());
         }
         const size_t nn = tree.nodes.size(), np = tree.prim_idx.size();
@@ -235,29 +275,6 @@ int build_scene(rt_renderer* r) {
         in.builder = RT_BUILDER_HOST;
         memcpy(rmin, tree.rmin, sizeof(rmin));
         memcpy(rmax, tree.rmax, sizeof(rmax));
-    } else {
-        GpuBuildResult res;
-        hipError_t e = r->gpu_build.build(r->d_spheres.p, n, p.min, p.max, depth, cap, r->stream, &res);
-        if (res.ref_overflow)
-            return fail(r, RT_E_INVALID,
-                        "scene too large for the octree: " + std::to_string(res.ref_overflow) +
-                            " sphere references in one level (limit 2^29); lower max_depth or "
-                            "raise leaf_capacity");
-        if (e != hipSuccess) return hip_fail(r, e, "device octree build");
-        if (res.n_invalid)
-            return fail(r, RT_E_INVALID, "scene has spheres with radius <= 0 or non-finite values");
-        sc.nodes = r->gpu_build.nodes();
-        sc.prim_sp = r->gpu_build.prim_sp();
-        sc.prim_idx = r->gpu_build.prim_idx();
-        sc.root = res.root;
-        sc.root_is_leaf = res.root_is_leaf ? 1u : 0u;
-        in.n_nodes = res.n_nodes;
-        in.n_leaves = res.n_leaves;
-        in.n_prim_refs = res.n_prims;
-        in.depth_reached = res.depth_reached;
-        in.builder = RT_BUILDER_DEVICE;
-        memcpy(rmin, res.rmin, sizeof(rmin));
-        memcpy(rmax, res.rmax, sizeof(rmax));
     }
     {
         // depth-K cell table over the tree (flags bits 28..31: 0 auto, 15 off, else K)
@@ -359,10 +376,26 @@ void accum_pixels(rt_renderer* r, const uint32_t* ids, uint32_t n, uint32_t ts) 
     r->accum_sig = sig;
 }
 
+// Order work about to be queued on `st` after the renderer's last queued work
+// when that ran on another stream (caller streams are typically non-blocking).
+int order_after_last(rt_renderer* r, hipStream_t st) {
+    if (r->pending && r->last_stream != st) RT_HIP(r, hipStreamWaitEvent(st, r->done, 0));
+    return RT_OK;
+}
+
+int mark_queued(rt_renderer* r, hipStream_t st) {
+    RT_HIP(r, hipEventRecord(r->done, st));
+    r->last_stream = st;
+    r->pending = true;
+    return RT_OK;
+}
+
 int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : r->stream;
     if (r->cfg.mode == RT_MODE_SCENE && !r->has_scene)
         return fail(r, RT_E_NOSCENE, "RT_MODE_SCENE render without rt_set_scene");
+    int ost;
+    if ((ost = order_after_last(r, st))) return ost;
     RT_HIP(r, hipMemsetAsync(r->counters.p, 0, kCounterWords * sizeof(unsigned long long), st));
     a.count_work = stats ? 1u : 0u;
     if (stats) RT_HIP(r, hipEventRecord(r->ev0, st));
@@ -381,6 +414,7 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
 #endif
     hipError_t e = r->cfg.mode == RT_MODE_SCENE ? launch_scene(a, st) : launch_compat(a, st);
     if (e != hipSuccess) return hip_fail(r, e, "kernel launch");
+    if ((ost = mark_queued(r, st))) return ost;
 #ifdef RT_TIMELINE
     if (tl_file) {
         std::vector<unsigned long long> h(tl_words);
@@ -470,6 +504,10 @@ int rt_create(const rt_config* cfg, rt_renderer** out) {
         return fail(nullptr, RT_E_INVALID, "rt_create: width/height out of range");
     if (cfg->mode != RT_MODE_COMPAT && cfg->mode != RT_MODE_SCENE)
         return fail(nullptr, RT_E_INVALID, "rt_create: unknown mode");
+    if (!variant_available((cfg->flags >> RT_FLAG_VARIANT_SHIFT) & 0xFu))
+        return fail(nullptr, RT_E_INVALID,
+                    "rt_create: scene-kernel variant not in this build (A/B variants need the "
+                    "-DRT_AB_VARIANTS library, make ab)");
     rt_renderer* r = new (std::nothrow) rt_renderer();
     if (!r) return fail(nullptr, RT_E_NOMEM, "rt_create: out of host memory");
     r->cfg = *cfg;
@@ -491,6 +529,7 @@ int rt_create(const rt_config* cfg, rt_renderer** out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&r->ev0);
     if (e == hipSuccess) e = hipEventCreate(&r->ev1);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&r->done, hipEventDisableTiming);
     if (e != hipSuccess) {
         st = hip_fail(nullptr, e, "rt_create");
         rt_destroy(r);
@@ -524,6 +563,7 @@ int rt_destroy(rt_renderer* r) {
     if (!r) return RT_OK;
     (void)hipSetDevice(r->device);
     if (r->stream) (void)hipStreamSynchronize(r->stream);
+    if (r->pending) (void)hipEventSynchronize(r->done);  // work on a caller's stream
     r->fb.release();
     r->rad.release();
     r->accum.release();
@@ -538,6 +578,7 @@ int rt_destroy(rt_renderer* r) {
     r->cell_table.release();
     if (r->ev0) (void)hipEventDestroy(r->ev0);
     if (r->ev1) (void)hipEventDestroy(r->ev1);
+    if (r->done) (void)hipEventDestroy(r->done);
     if (r->stream) (void)hipStreamDestroy(r->stream);
     delete r;
     return RT_OK;
@@ -774,6 +815,7 @@ int rt_render_tiles(rt_renderer* r, const uint32_t* tile_ids, uint32_t n_tiles, 
         return RT_OK;
     }
     const uint32_t* dev_ids = nullptr;
+    if ((st = order_after_last(r, s))) return st;
     if ((st = tile_list(r, tile_ids, n_tiles, s, &dev_ids))) return st;
     accum_pixels(r, tile_ids, n_tiles, ts);
     FrameArgs a;
@@ -808,11 +850,12 @@ int rt_unpack_tiles(rt_renderer* r, const void* dev_packed, const uint32_t* tile
     if ((st = set_device(r))) return st;
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->stream;
     const uint32_t* dev_ids = nullptr;
+    if ((st = order_after_last(r, s))) return st;
     if ((st = tile_list(r, tile_ids, n_tiles, s, &dev_ids))) return st;
     hipError_t e = launch_unpack(static_cast<const uint32_t*>(dev_packed), dev_ids, n_tiles, ts, tx,
                                  r->W, r->H, dev_rgba8 ? static_cast<uint32_t*>(dev_rgba8) : r->fb.p, s);
     if (e != hipSuccess) return hip_fail(r, e, "rt_unpack_tiles");
-    return RT_OK;
+    return mark_queued(r, s);
 }
 
 int rt_reset_accumulation(rt_renderer* r) {
@@ -826,6 +869,7 @@ int rt_synchronize(rt_renderer* r) {
     int st;
     if ((st = set_device(r))) return st;
     RT_HIP(r, hipStreamSynchronize(r->stream));
+    if (r->pending) RT_HIP(r, hipEventSynchronize(r->done));
     return RT_OK;
 }
 
@@ -833,7 +877,9 @@ int rt_readback(rt_renderer* r, uint8_t* host_rgba8, float* host_rgba32f) {
     if (!r) return RT_E_INVALID;
     int st;
     if ((st = set_device(r))) return st;
+    // the frame may have been queued on a caller's stream
     RT_HIP(r, hipStreamSynchronize(r->stream));
+    if (r->pending) RT_HIP(r, hipEventSynchronize(r->done));
     const size_t px = (size_t)r->W * r->H;
     if (host_rgba8) RT_HIP(r, hipMemcpy(host_rgba8, r->fb.p, px * 4, hipMemcpyDeviceToHost));
     if (host_rgba32f) {

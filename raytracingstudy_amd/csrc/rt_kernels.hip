@@ -217,6 +217,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
     // kSmemLeaf / kLaneLeaf are measured alternatives for wave-uniform leaves
     // (variants 14-16), none faster.
     auto leaf = [&](uint32_t off, uint32_t cnt) -> bool {
+#ifdef RT_AB_VARIANTS
         if (kLdsLeaf) {
             // Wave-uniform leaf (the usual case: the lanes are one pixel's
             // samples): the active lanes fetch the leaf's spheres once, one
@@ -299,6 +300,9 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 return false;
             }
         }
+#else
+        static_assert(!kLdsLeaf && !kSmemLeaf && !kLaneLeaf, "leaf modes are A/B builds (-DRT_AB_VARIANTS)");
+#endif
         const float4* __restrict__ ps = prim_sp + off;
         static_assert(kChunk <= kPrimPad + 1, "leaf loads may run kChunk-1 spheres past a leaf");
         for (uint32_t j = 0; j < cnt; j += kChunk) {
@@ -462,6 +466,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
     return false;
 }
 
+#ifdef RT_AB_VARIANTS
 // ---------------------------------------------------------------------------
 // Packet variant: the wave walks the octree as ONE 64-ray packet.
 //
@@ -655,6 +660,7 @@ __device__ __forceinline__ bool walk_packet(const SceneArgs& S, bool want, float
     }
     return false;
 }
+#endif  // RT_AB_VARIANTS (packet walk)
 
 // ---------------------------------------------------------------------------
 // Frame mapping, shading, ordered accumulation
@@ -703,6 +709,7 @@ __device__ __forceinline__ void flush_counters(const FrameArgs& a, uint32_t prim
     }
 }
 
+#ifdef RT_AB_VARIANTS
 // One sample of pixel (x, y): primary walk, Lambert shade, shadow walk.
 // kVar selects the traversal; `valid` lanes trace, the others only take part
 // in the packet walks' wave-wide votes.
@@ -772,6 +779,7 @@ __device__ __forceinline__ PixelOut sample_color(const FrameArgs& a, uint32_t x,
     }
     return c;
 }
+#endif  // RT_AB_VARIANTS (separate primary/shadow walks)
 
 // Unified lane path: one walk instance run twice (primary, then the shadow ray
 // of the lanes that need one), so the register allocator sees one walk.
@@ -878,11 +886,17 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
         const uint32_t sg = r * spw + sub_base;
         const bool valid = lane_ok && sg < s_end;
         n_primary += static_cast<uint32_t>(__popcll(__ballot(valid)));  // wave-uniform
+#ifdef RT_AB_VARIANTS
         PixelOut c = kVar == kVariantLaneUnified
                          ? sample_color_unified<kChunk, kStats, kLeafMode>(
                                a, x, y, hp, sg, valid, n_shadow, n_nodes, n_prims, stk, lbuf)
                          : sample_color<kVar, kChunk>(a, x, y, hp, sg, valid, n_shadow,
                                                             n_nodes, n_prims, stk);
+#else
+        static_assert(kVar == kVariantLaneUnified, "other walks are A/B builds (-DRT_AB_VARIANTS)");
+        PixelOut c = sample_color_unified<kChunk, kStats, kLeafMode>(
+            a, x, y, hp, sg, valid, n_shadow, n_nodes, n_prims, stk, lbuf);
+#endif
         // Pixel sum of this round: pairwise butterfly over the pixel's g
         // lanes (missing samples are 0) = oracle.c:tree_sum; rounds are then
         // added in order in the leader's LDS slot.
@@ -942,11 +956,11 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     float4* acc = lds;  // [256] running pixel sums (leader lanes' slots)
     const uint32_t wave = threadIdx.x >> 6;
-    void* stk;
+    void* stk = reinterpret_cast<uint2*>(lds + kBlockThreads) + threadIdx.x;
+#ifdef RT_AB_VARIANTS
     if (kVar == kVariantPacket)
         stk = reinterpret_cast<PStackEntry*>(lds + kBlockThreads) + wave * a.stack_entries;
-    else
-        stk = reinterpret_cast<uint2*>(lds + kBlockThreads) + threadIdx.x;
+#endif
     // per-wave leaf buffer after the ancestor stacks (scene_lds_bytes)
     float4* lbuf = nullptr;
     if (kLeafMode == 1) {
@@ -1105,8 +1119,10 @@ hipError_t launch_compat(const FrameArgs& a, hipStream_t st) {
 
 size_t scene_lds_bytes(const FrameArgs& a) {
     const size_t colours = kBlockThreads * sizeof(float4);  // pixel sums
+#ifdef RT_AB_VARIANTS
     if (a.variant == kVariantPacket)
         return colours + static_cast<size_t>(a.stack_entries) * (kBlockThreads / 64) * sizeof(PStackEntry);
+#endif
     const uint32_t levels = stack_levels(a.sc);
     const size_t leafbuf = a.variant == kVariantWaveQLds
                                ? static_cast<size_t>(kBlockThreads / 64) * kLeafBuf * sizeof(float4)
@@ -1226,46 +1242,62 @@ static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStr
         return;
     }
     switch (a.variant) {
+        case kVariantLaneUnified:  // the spp < 8 default (block-tile queue)
+            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2>, a, n_bt, lds, st);
+            break;
+        case kVariantLaneUnified2NoStats:  // 7 with counters only in stats frames
+            if (a.count_work)
+                launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true>, a, n_bt,
+                                  lds, st);
+            else
+                launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false>, a,
+                                  n_bt, lds, st);
+            break;
+        case kVariantWaveQ:  // the spp >= 8 default: per-wave scheduling over per-XCD queues,
+            // 7 waves/SIMD (C3 -2.8%, C5 -5.4% against 6 waves, profiles/r01/occupancy_ab.log)
+            if (a.count_work)
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, true, false, true>,
+                             a, lds, st);
+            else
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, false, false, true>,
+                             a, lds, st);
+            break;
+#ifdef RT_AB_VARIANTS
+        // measured-and-rejected alternatives, A/B builds only
         case kVariantPacket:
             launch_persistent(scene_kernel<kTiles, kVariantPacket, 1, 4>, a, n_bt, lds, st);
             break;
         case kVariantLaneChunk2:
             launch_persistent(scene_kernel<kTiles, kVariantLane, 1, 2>, a, n_bt, lds, st);
             break;
-        case kVariantLaneUnified:
-            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2>, a, n_bt, lds, st);
+        case kVariantLane:
+            launch_persistent(scene_kernel<kTiles, kVariantLane, 1, 4>, a, n_bt, lds, st);
             break;
         case kVariantWaveQLds:  // 13 + wave-uniform leaves staged through LDS
             if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true,
-                                          1>,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true, 1>,
                              a, lds, st);
             else
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true,
-                                          1>,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true, 1>,
                              a, lds, st);
             break;
         case kVariantWaveQLane:  // 13 + one-lane loads broadcast by readfirstlane
             if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true,
-                                          3>,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true, 3>,
                              a, lds, st);
             else
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true,
-                                          3>,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true, 3>,
                              a, lds, st);
             break;
         case kVariantWaveQSmem:  // 13 + wave-uniform leaves read by scalar loads
             if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true,
-                                          2>,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true, 2>,
                              a, lds, st);
             else
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true,
-                                          2>,
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true, 2>,
                              a, lds, st);
             break;
-        case kVariantWaveQ6:  // 13 at the allocator's own occupancy (6 waves/SIMD, no VGPR spills)
+        case kVariantWaveQ6:  // 13 at the allocator's own occupancy (6 waves/SIMD)
             if (a.count_work)
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true>,
                              a, lds, st);
@@ -1281,28 +1313,23 @@ static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStr
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 8, 2, false, false, true>,
                              a, lds, st);
             break;
-        case kVariantWaveQ:  // per-wave scheduling over per-XCD queues, 7 waves/SIMD
-            // (72 VGPRs; the few VGPR spills are per pixel, outside the walk
-            // loop: C3 -2.8%, C5 -5.4% against 6 waves, profiles/r01/occupancy_ab.log)
-            if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, true, false, true>,
-                             a, lds, st);
-            else
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, false, false, true>,
-                             a, lds, st);
-            break;
-        case kVariantLaneUnified2NoStats:  // A/B only: variant 7 without the work counters
-            if (a.count_work)
-                launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true>, a, n_bt,
-                                  lds, st);
-            else
-                launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false>, a,
-                                  n_bt, lds, st);
-            break;
-        default:
-            launch_persistent(scene_kernel<kTiles, kVariantLane, 1, 4>, a, n_bt, lds, st);
+#endif
+        default:  // rejected by variant_available() before any launch
             break;
     }
+}
+
+// Variants compiled into this build (rt_create refuses the others).
+bool variant_available(uint32_t v) {
+    if (v == 0 || v == kVariantLaneUnified || v == kVariantLaneUnified2NoStats || v == kVariantWaveQ)
+        return true;
+#ifdef RT_AB_VARIANTS
+    return v == kVariantLane || v == kVariantPacket || v == kVariantLaneChunk2 ||
+           v == kVariantWaveQLds || v == kVariantWaveQSmem || v == kVariantWaveQLane ||
+           v == kVariantWaveQ6 || v == kVariantWaveQ8;
+#else
+    return false;
+#endif
 }
 
 hipError_t launch_scene(const FrameArgs& a_in, hipStream_t st) {

@@ -30,7 +30,9 @@ constexpr uint32_t kVariantWaveQ6 = 8;     // 13 at 6 waves/SIMD, no spills (A/B
 constexpr uint32_t kVariantWaveQ8 = 9;     // 13 compiled for 8 waves/SIMD (A/B)
 constexpr uint32_t kPrimPad = 4;           // prim_sp padding: scalar reads may run 3 past a leaf
 
-// A/B toggles (rt_config.flags bits 20..23), results identical either way
+// A/B toggles (rt_config.flags bits 20..27), results identical either way
+constexpr uint32_t kOptDeviceBuildRefuse = 1u << 0;  // bit 0: treat every tree as too large for
+                                                     // the device builder (tests its host fallback)
 constexpr uint32_t kOptBtsShift = 1;       // bits 1..3: force the block-tile side (A/B):
                                            // 0 auto, 1 = 16, 2 = 8, 3 = 4, 4 = 2 pixels
 constexpr uint32_t kOptNoWgCap = 1u << 7; // bit 7: 1-spp frames without the 3-workgroups-per-CU cap

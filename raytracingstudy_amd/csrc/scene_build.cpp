@@ -5,6 +5,7 @@
 // min 0, max 1.28, resolution 0.01 at src/renderer.cu:134-138) and traverse()
 // is a stub.  This builder defines the structure the render kernel walks;
 // the semantics are specified in DESIGN.md "Octree build".
+#include <stdexcept>
 #include "scene_build.h"
 
 #include <math.h>
@@ -168,6 +169,9 @@ void build_octree(const float* spheres, uint32_t n, const float rmin[3], const f
         std::vector<Cell> next;
         for (Cell& cell : level) {
             if (is_leaf(cell)) {
+                // leaf offsets are 32-bit record fields (+ the kPrimPad tail)
+                if (out.prim_idx.size() + cell.list.size() + 4u >= (size_t(1) << 32))
+                    throw std::length_error("more than 2^32 - 5 leaf references");
                 const uint32_t off = static_cast<uint32_t>(out.prim_idx.size());
                 for (uint32_t idx : cell.list) {
                     out.prim_idx.push_back(idx);
@@ -194,6 +198,8 @@ void build_octree(const float* spheres, uint32_t n, const float rmin[3], const f
                 valid |= 1u << ch;
                 if (is_leaf(k)) leafm |= 1u << ch;
             }
+            if (out.nodes.size() + 8u >= (size_t(1) << 32))
+                throw std::length_error("more than 2^32 - 9 node records");
             const uint32_t first = static_cast<uint32_t>(out.nodes.size());
             out.nodes[cell.slot] = {first, valid | (leafm << 8)};
             for (uint32_t ch = 0; ch < 8; ++ch) {

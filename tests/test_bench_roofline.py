@@ -1,0 +1,63 @@
+"""bench.py's roofline block (CPU): every roof comes from measured data, a
+fraction above 1 is never reported, and algorithmic (cache-served) bytes are
+never priced against HBM."""
+import json
+import os
+
+import pytest
+
+import bench
+from raytracingstudy_amd._lib import kernel_source_id
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PMC = os.path.join(ROOT, "profiles", "pmc_latest.json")
+SIMDS = 1024  # 256 CUs x 4 SIMDs
+
+
+def _pmc():
+    with open(PMC) as f:
+        return json.load(f)
+
+
+def test_valu_issue_is_the_bound_when_hbm_traffic_is_tiny():
+    pmc = _pmc()
+    kern_ms = pmc["scene_kernel_avg_ns"] / 1e6
+    # C3 touches ~182 GB of node/sphere records per launch:
+    # more than HBM could move in that time, so it must not be an HBM fraction
+    touched = 182.19e9
+    r = bench.roofline(kern_ms, touched, pmc, SIMDS)
+    assert r["frac"] is not None and 0 < r["frac"] <= 1.0
+    assert r["traffic"] / touched < 0.01
+    assert r["bound"] != "hbm" and r["bound"] == "valu_issue"
+    v = r["roofs"]["valu_issue"]
+    insts = pmc["sq"]["SQ_INSTS_VALU"]
+    peak = SIMDS * pmc["effective_clock_ghz"] / 2.0  # G wave-instructions / s
+    assert v["frac"] == pytest.approx(insts / (kern_ms / 1e3) / 1e9 / peak, rel=1e-3)
+    assert all(x["frac"] <= 1.0 for k, x in r["roofs"].items() if k == r["bound"])
+
+
+def test_over_unity_roofs_are_never_chosen():
+    pmc = dict(_pmc())
+    pmc["sq"] = dict(pmc["sq"], SQ_INSTS_VALU=pmc["sq"]["SQ_INSTS_VALU"] * 5)  # impossible rate
+    r = bench.roofline(pmc["scene_kernel_avg_ns"] / 1e6, 1e9, pmc, SIMDS)
+    assert r["roofs"]["valu_issue"]["frac"] > 1.0
+    assert r["bound"] != "valu_issue" and (r["frac"] is None or r["frac"] <= 1.0)
+
+
+def test_without_pmc_only_the_cache_roof_remains():
+    r = bench.roofline(12.0, 182.19e9, None, SIMDS, pmc_note="stale")
+    assert r["bound"] == "l2" and r["frac"] <= 1.0 and r["traffic"] is None
+    assert r["pmc"] == "stale" and "hbm" not in r["roofs"]
+
+
+def test_stale_pmc_summary_is_refused(tmp_path):
+    pmc = dict(_pmc(), kernel_source_id="0000000000000000")
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps(pmc))
+    ent, why = bench.load_pmc(str(p), pmc["config"], 1, kernel_source_id())
+    assert ent is None and "stale" in why
+    pmc["kernel_source_id"] = kernel_source_id()
+    p.write_text(json.dumps(pmc))
+    ent, why = bench.load_pmc(str(p), pmc["config"], 1, kernel_source_id())
+    assert ent is not None and why == "ok"
+    assert bench.load_pmc(str(p), "c5", 1, kernel_source_id())[0] is None

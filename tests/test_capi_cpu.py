@@ -133,12 +133,16 @@ def test_gl_interop_header_compiles(tmp_path):
 
 def test_committed_pmc_summary_feeds_the_bench_roofline():
     """bench.py reads profiles/pmc_latest.json (tools/pmc_traffic.py output) for
-    `roofline.traffic` and `roofline.valu_issue`; a format drift would silently
-    null them in the round-end bench line."""
+    the VALU-issue and HBM roofs.  It must be stamped with THIS build's kernel
+    sources (re-run tools/profile.sh after every kernel change and copy the
+    summary), or the round-end bench line falls back to the cache roof."""
     import bench
+    from raytracingstudy_amd._lib import kernel_source_id
     path = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    traffic, valu = bench.pmc_figures(path, "c3", 1, 13.5, 1024)
-    assert traffic and traffic > 0
-    assert valu and 0.0 < valu["frac"] < 1.0
-    assert bench.pmc_figures(path, "c5", 1, 13.5, 1024) == (None, None)
-    assert bench.pmc_figures(path, "c3", 2, 13.5, 1024) == (None, None)
+    ent, why = bench.load_pmc(path, "c3", 1, kernel_source_id())
+    assert ent is not None, why
+    r = bench.roofline(ent["scene_kernel_avg_ns"] / 1e6, 182e9, ent, 1024)
+    assert r["bound"] == "valu_issue" and 0.0 < r["frac"] <= 1.0
+    assert r["traffic"] and r["traffic"] > 0
+    assert bench.load_pmc(path, "c5", 1, kernel_source_id())[0] is None
+    assert bench.load_pmc(path, "c3", 2, kernel_source_id())[0] is None

@@ -7,7 +7,7 @@ HBM traffic follows MI355X_MICROARCH.md "HBM": FETCH_SIZE / WRITE_SIZE are in
 KiB and come from separate --pmc passes; on gfx950 FETCH_SIZE reports half the
 bytes of wide coalesced reads, so the corrected read bytes are 2 x FETCH_SIZE
 (the raw sum is reported beside it; the guide notes other access widths are
-uncalibrated).  Counters are averaged over every dispatch of the scene kernel.
+uncalibrated).  Counters are the median over the scene kernel's dispatches (the timed frames).
 """
 from __future__ import annotations
 
@@ -27,13 +27,22 @@ def _rows(pattern):
     return out
 
 
+def _median(xs):
+    xs = sorted(xs)
+    n = len(xs)
+    return xs[n // 2] if n % 2 else 0.5 * (xs[n // 2 - 1] + xs[n // 2])
+
+
 def counters(d, kernel_sub="scene_kernel"):
+    """Per counter: (median over dispatches, dispatches).  The median, because
+    the bench's first dispatch is its stats frame (the work-counting build,
+    ~8% more VALU) and every later one is the timed counter-free build."""
     per = defaultdict(lambda: defaultdict(float))
     for r in _rows(os.path.join(d, "**", "*counter_collection.csv")):
         if kernel_sub not in r.get("Kernel_Name", ""):
             continue
         per[r["Counter_Name"]][r.get("Dispatch_Id", r.get("Correlation_Id"))] += float(r["Counter_Value"])
-    return {k: (sum(v.values()) / len(v), len(v)) for k, v in per.items() if v}
+    return {k: (_median(list(v.values())), len(v)) for k, v in per.items() if v}
 
 
 def kernel_stats(d):
@@ -54,13 +63,17 @@ def trace_durations(d, kernel_sub="scene_kernel"):
 
 def main():
     root, cfg = sys.argv[1], sys.argv[2]
-    res = {"config": cfg, "n_gpus": 1}
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from raytracingstudy_amd._lib import kernel_source_id
+    # stamp: bench.py takes these counters only while the kernel sources match
+    res = {"config": cfg, "n_gpus": 1, "kernel_source_id": kernel_source_id()}
     ks = kernel_stats(os.path.join(root, "trace"))
     res["kernel_stats"] = ks
     durs = trace_durations(os.path.join(root, "trace"))
     if durs:
         res["scene_kernel_dispatches"] = len(durs)
         res["scene_kernel_avg_ns"] = sum(durs) / len(durs)
+        res["scene_kernel_median_ns"] = _median(durs)
     f = counters(os.path.join(root, "fetch")).get("FETCH_SIZE")
     w = counters(os.path.join(root, "write")).get("WRITE_SIZE")
     if f and w:
@@ -79,7 +92,7 @@ def main():
         if cyc:
             res["valu_active_frac_of_wave_cycles"] = act / cyc
         if gui and durs:
-            res["effective_clock_ghz"] = gui / 8.0 / (sum(durs) / len(durs))
+            res["effective_clock_ghz"] = gui / 8.0 / _median(durs)
         if waves:
             res["valu_insts_per_wave"] = sq.get("SQ_INSTS_VALU", (0, 0))[0] / waves
     print(json.dumps(res, indent=1))
