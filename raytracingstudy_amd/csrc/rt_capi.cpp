@@ -412,8 +412,34 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
         a.timeline = tl;
     }
 #endif
+#ifdef RT_BLOCK_STATS
+    // diagnostic build (tools/block_stats.py): stats frames count the wave
+    // executions of every walk block and append them to $RT_BLOCK_STATS_FILE
+    static unsigned long long* bsd = nullptr;
+    const char* bs_file = stats ? getenv("RT_BLOCK_STATS_FILE") : nullptr;
+    a.bstats = nullptr;
+    if (bs_file) {
+        if (!bsd) RT_HIP(r, hipMalloc(reinterpret_cast<void**>(&bsd), 2 * kBlockStats * 8));
+        RT_HIP(r, hipMemsetAsync(bsd, 0, 2 * kBlockStats * 8, st));
+        a.bstats = bsd;
+    }
+#endif
     hipError_t e = r->cfg.mode == RT_MODE_SCENE ? launch_scene(a, st) : launch_compat(a, st);
     if (e != hipSuccess) return hip_fail(r, e, "kernel launch");
+#ifdef RT_BLOCK_STATS
+    if (bs_file) {
+        unsigned long long h[2 * kBlockStats];
+        RT_HIP(r, hipStreamSynchronize(st));
+        RT_HIP(r, hipMemcpy(h, bsd, sizeof(h), hipMemcpyDeviceToHost));
+        if (FILE* f = fopen(bs_file, "a")) {
+            fprintf(f, "{\"W\": %u, \"H\": %u, \"spp\": %u, \"counts\": [", a.W, a.H, a.spp);
+            for (uint32_t i = 0; i < 2 * kBlockStats; ++i)
+                fprintf(f, "%s%llu", i ? ", " : "", h[i]);
+            fprintf(f, "]}\n");
+            fclose(f);
+        }
+    }
+#endif
     if ((ost = mark_queued(r, st))) return ost;
 #ifdef RT_TIMELINE
     if (tl_file) {

@@ -110,11 +110,27 @@ __global__ void __launch_bounds__(kBlockThreads) compat_tiles_kernel(FrameArgs a
 // Scene mode
 // ---------------------------------------------------------------------------
 
+#ifdef RT_BLOCK_STATS
+// Diagnostic build: the first active lane counts one execution of block i by
+// the wave, and the active lanes (BlockStat, rt_params.h).
+__device__ __forceinline__ void bs_count(uint32_t* bs, uint32_t i) {
+    const uint64_t m = __ballot(1);
+    if (__lane_id() == static_cast<uint32_t>(__builtin_ctzll(m))) {
+        bs[2 * i] += 1u;
+        bs[2 * i + 1] += static_cast<uint32_t>(__popcll(m));
+    }
+}
+#define RT_BS(i) bs_count(bs, (i))
+#else
+#define RT_BS(i) ((void)0)
+#endif
+
 // Nearest root with the perpendicular-distance discriminant, explicit FMAs
 // (13 VALU to the h < 0 test); accepted iff tmin < t < tmax.  Same operations
 // as oracle.c:isect.
 __device__ __forceinline__ bool isect(float o0, float o1, float o2, float d0, float d1, float d2,
-                                      float4 sp, float tmin, float tmax, float& tout) {
+                                      float4 sp, float tmin, float tmax, float& tout,
+                                      uint32_t* bs = nullptr) {
     const float ocx = o0 - sp.x;
     const float ocy = o1 - sp.y;
     const float ocz = o2 - sp.z;
@@ -125,12 +141,52 @@ __device__ __forceinline__ bool isect(float o0, float o1, float o2, float d0, fl
     const float qq = fmaf(qz, qz, fmaf(qy, qy, qx * qx));
     const float h = fmaf(sp.w, sp.w, -qq);
     if (h < 0.0f) return false;
+    RT_BS(kBsSqrt);
     const float sq = sqrtf(h);
     float t = -b - sq;
     if (!(t > tmin)) t = -b + sq;
     if (!(t > tmin) || !(t < tmax)) return false;
     tout = t;
     return true;
+}
+
+// v_readlane of a float's bits (the builtin is int-typed: a float argument
+// would be converted to an integer value)
+__device__ __forceinline__ float readlane_f(float x, uint32_t lane) {
+    return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(x), lane));
+}
+
+// Ray bundle of one walk phase (DESIGN.md 5.1 "Bundle prefilter"): the wave's
+// rays lie within A (origins) and B (unit directions) of a reference ray
+// (o, d) taken from one of its lanes.  For a sphere (c, r) with perpendicular
+// distance D* from the reference line, every lane's line is at least
+// D* - A - (|c - o| + A) B away, and |c - o| <= |b| + D* (b = (c - o).d), so
+// no lane's discriminant can be >= 0 unless
+//     D* <= R = (r + eps + A + (|b| + A) B) / (1 - B),   B <= 1/2,
+// evaluated as (r + c0 + |b| c1) * c2 with 1/(1 - B) <= 1 + 2B.  eps =
+// kBundleEps (1 + |b| + A) is orders of magnitude above the float error of
+// both the lanes' h and this test.  Spheres failing it are skipped for the
+// whole wave; the others get the lanes' exact isect, in list order.
+constexpr float kBundleEps = 1.0f / 16384.0f;
+struct Bundle {
+    float o0, o1, o2, d0, d1, d2;
+    float c0, c1, c2;  // c0 = eps (1 + A) + A + A B, c1 = eps + B, c2 = 1 + 2B
+    bool ok;           // false: per-lane leaf tests (non-finite or too wide bundle)
+};
+
+// isect's discriminant h alone (same operations): h < 0 <=> isect rejects
+// the sphere before its square root.
+__device__ __forceinline__ float isect_h(float o0, float o1, float o2, float d0, float d1,
+                                         float d2, float4 sp) {
+    const float ocx = o0 - sp.x;
+    const float ocy = o1 - sp.y;
+    const float ocz = o2 - sp.z;
+    const float b = fmaf(ocz, d2, fmaf(ocy, d1, ocx * d0));
+    const float qx = fmaf(-b, d0, ocx);
+    const float qy = fmaf(-b, d1, ocy);
+    const float qz = fmaf(-b, d2, ocz);
+    const float qq = fmaf(qz, qz, fmaf(qy, qy, qx * qx));
+    return fmaf(sp.w, sp.w, -qq);
 }
 
 // Ancestor-stack levels per thread: depths 1..D-1, or K..D-1 with a cell table
@@ -149,12 +205,14 @@ __host__ __device__ inline uint32_t stack_levels(const SceneArgs& S) {
 // kAnyHit: compile-time any-hit; with kDynAny the mode comes from `any_rt`
 // instead, so ONE inlined walk serves both the primary and the shadow ray.
 template <bool kAnyHitT, int kChunk = 4, bool kDynAny = false, bool kStats = true,
-          bool kLdsLeaf = false, bool kSmemLeaf = false, bool kLaneLeaf = false>
+          bool kLdsLeaf = false, bool kSmemLeaf = false, bool kLaneLeaf = false,
+          bool kBundle = false>
 __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, float o2, float d0,
                                      float d1, float d2, float tmin, float tmax, float& tout,
                                      uint32_t& iout, uint32_t& n_nodes, uint32_t& n_prims,
                                      uint2* __restrict__ stk, bool any_rt = false,
-                                     float4* __restrict__ lbuf = nullptr) {
+                                     float4* __restrict__ lbuf = nullptr, uint32_t* bs = nullptr,
+                                     const Bundle* bun = nullptr) {
     const bool kAnyHit = kDynAny ? any_rt : kAnyHitT;
     const uint32_t D = S.max_depth;
     const uint32_t G = 1u << D;
@@ -187,6 +245,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
     if (t0 < tmin) t0 = tmin;
     if (t1 > tmax) t1 = tmax;
     if (!(t0 < t1)) return false;
+    RT_BS(kBsWalk);
 
     float best_t = tmax;
     if (kStats) n_nodes += 1;
@@ -197,8 +256,10 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
     uint32_t best_ref = kNoHit;
     auto test = [&](const float4& sp, uint32_t ref) -> bool {
         if (kStats) n_prims += 1;
+        RT_BS(kBsTest);
         float th;
-        if (isect(o0, o1, o2, d0, d1, d2, sp, tmin, tmax, th)) {
+        if (isect(o0, o1, o2, d0, d1, d2, sp, tmin, tmax, th, bs)) {
+            RT_BS(kBsAccept);
             if (kAnyHit) {
                 tout = th;
                 return true;
@@ -216,7 +277,87 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
     // oracle): each lane loads its own, kChunk loads in flight.  kLdsLeaf /
     // kSmemLeaf / kLaneLeaf are measured alternatives for wave-uniform leaves
     // (variants 14-16), none faster.
+    // Bundle-prefiltered leaf (kBundle): the lanes in this block share out the
+    // leaf's spheres (lane of rank k loads sphere k), test each against the
+    // wave's ray bundle, and only the spheres some lane could hit are then
+    // tested exactly by every lane of the leaf, in list order.  Lanes in other
+    // leaves are served leaf by leaf (first pending lane's leaf first).  Same
+    // spheres accepted, same order, same results as the per-lane loop below.
+    auto leaf_bundle = [&](uint32_t off, uint32_t cnt) -> bool {
+        bool pending = true, found = false;
+        for (;;) {
+            const uint64_t pm = __ballot(pending);
+            if (pm == 0) break;
+            const uint32_t lead = static_cast<uint32_t>(__builtin_ctzll(pm));
+            const uint32_t uoff = __builtin_amdgcn_readlane(off, lead);
+            const uint32_t ucnt = __builtin_amdgcn_readlane(cnt, lead);
+            const bool mine = pending && off == uoff;
+            RT_BS(kBsLeaf);
+            const uint64_t ex = __ballot(1);
+            const uint32_t nact = static_cast<uint32_t>(__popcll(ex));
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                static_cast<uint32_t>(ex >> 32),
+                __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(ex), 0u));
+            uint32_t hit_at = ucnt;  // list position of this lane's any-hit
+            for (uint32_t base = 0; base < ucnt; base += nact) {
+                RT_BS(kBsLeafChunk);
+                const uint32_t j = base + rank;
+                float4 sp;  // lanes past the leaf's end never become candidates
+                bool pass = false;
+                if (j < ucnt) {
+                    sp = prim_sp[uoff + j];
+                    const float ox = sp.x - bun->o0, oy = sp.y - bun->o1, oz = sp.z - bun->o2;
+                    const float b = fmaf(oz, bun->d2, fmaf(oy, bun->d1, ox * bun->d0));
+                    const float qx = fmaf(-b, bun->d0, ox);
+                    const float qy = fmaf(-b, bun->d1, oy);
+                    const float qz = fmaf(-b, bun->d2, oz);
+                    const float qq = fmaf(qz, qz, fmaf(qy, qy, qx * qx));
+                    const float R = fmaf(fabsf(b), bun->c1, sp.w + bun->c0) * bun->c2;
+                    pass = qq <= R * R;
+                }
+                uint64_t cm = __ballot(pass);
+                while (cm) {
+                    const uint32_t L = static_cast<uint32_t>(__builtin_ctzll(cm));
+                    cm &= cm - 1u;
+                    float4 c;
+                    c.x = readlane_f(sp.x, L);
+                    c.y = readlane_f(sp.y, L);
+                    c.z = readlane_f(sp.z, L);
+                    c.w = readlane_f(sp.w, L);
+                    const uint32_t jj =
+                        base + static_cast<uint32_t>(__popcll(ex & ((1ull << L) - 1ull)));
+                    if (mine && !found) {
+                        RT_BS(kBsTest);
+                        float th;
+                        if (isect(o0, o1, o2, d0, d1, d2, c, tmin, tmax, th, bs)) {
+                            RT_BS(kBsAccept);
+                            const uint32_t ref = uoff + jj;
+                            if (kAnyHit) {
+                                tout = th;
+                                found = true;
+                                hit_at = jj;
+                            } else if (th < best_t) {
+                                best_t = th;
+                                best_ref = ref;
+                            } else if (th == best_t && S.prim_idx[ref] < S.prim_idx[best_ref]) {
+                                best_ref = ref;
+                            }
+                        }
+                    }
+                }
+            }
+            // counters as the per-lane loop counts them: every sphere of the
+            // leaf, or up to and including an any-hit
+            if (kStats && mine) n_prims += found ? hit_at + 1u : ucnt;
+            pending = pending && !mine;
+        }
+        return found;
+    };
     auto leaf = [&](uint32_t off, uint32_t cnt) -> bool {
+        // wave-uniform leaves only: lanes in different leaves are served
+        // concurrently by the per-lane loop below (one latency for all)
+        if (kBundle && bun->ok && __all(off == __builtin_amdgcn_readfirstlane(off)))
+            return leaf_bundle(off, cnt);
 #ifdef RT_AB_VARIANTS
         if (kLdsLeaf) {
             // Wave-uniform leaf (the usual case: the lanes are one pixel's
@@ -305,7 +446,9 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
 #endif
         const float4* __restrict__ ps = prim_sp + off;
         static_assert(kChunk <= kPrimPad + 1, "leaf loads may run kChunk-1 spheres past a leaf");
+        RT_BS(kBsLeaf);
         for (uint32_t j = 0; j < cnt; j += kChunk) {
+            RT_BS(kBsLeafChunk);
             const uint32_t m = cnt - j;
             // kChunk unconditional dwordx4 loads in flight at fixed offsets; a
             // slot past the leaf's end reads the next leaf or the array's
@@ -317,6 +460,23 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 // issue in list order, so the first test waits for its own
                 // sphere only (vmcnt(kChunk-1)), not for the whole chunk
                 __builtin_amdgcn_sched_barrier(0);
+            }
+            // Uniform screen: every lane's discriminants first, with no branch;
+            // only when some lane's h is >= 0 (or NaN) does the wave run the
+            // exact per-lane tests (which recompute them), one branch for the
+            // chunk instead of a divergent branch per test.  h < 0 is exactly
+            // where isect returns false, so the same spheres are accepted.
+            bool maybe = false;
+#pragma unroll
+            for (int q = 0; q < kChunk; ++q) {
+                // unconditional (a slot past the leaf's end holds a real
+                // sphere record too), masked without a branch
+                const bool pos = !(isect_h(o0, o1, o2, d0, d1, d2, sv[q]) < 0.0f);
+                maybe |= (m > static_cast<uint32_t>(q)) & pos;
+            }
+            if (!__any(maybe)) {
+                if (kStats) n_prims += min(m, static_cast<uint32_t>(kChunk));
+                continue;
             }
 #pragma unroll
             for (int q = 0; q < kChunk; ++q)
@@ -346,13 +506,16 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         // Hard cap (never reached by a correct walk: a ray crosses < 3*G cells
         // and each crossing costs at most one descent): no input can hang the GPU.
         for (uint32_t it = 0, cap = 8u * G + 64u; it < cap; ++it) {
+            RT_BS(kBsIter);
             uint2 rec;
             bool have;  // rec is a leaf record (else the cell is empty)
             if (jump) {
+                RT_BS(kBsJump);
                 jump = false;
                 // mid-plane tests at t from `depth` down to K (no loads: the
                 // descent's child choices), then the cell's table entry
                 while (depth < K) {
+                    RT_BS(kBsJumpDescend);
                     const uint32_t half = size >> 1;
                     l0 += plane(0, l0 + half) <= t ? half : 0u;
                     l1 += plane(1, l1 + half) <= t ? half : 0u;
@@ -383,6 +546,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 }
                 have = kind == kCellLeaf;
             } else {
+                RT_BS(kBsDescend);
                 const uint32_t half = size >> 1;
                 const bool b0 = plane(0, l0 + half) <= t;
                 const bool b1 = plane(1, l1 + half) <= t;
@@ -401,6 +565,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                     rec = nodes[slot];
                     if (kStats) n_nodes += 1;
                     if (!((node.y >> 8) & (1u << child))) {
+                        RT_BS(kBsInternal);
                         node = rec;
                         stk[(depth - 1 - sb) * kBlockThreads] = rec;
                         continue;
@@ -410,6 +575,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             if (have) {
                 if (leaf(rec.x, rec.y)) return true;
             }
+            RT_BS(kBsExit);
             const float e0 = plane(0, l0 + size);
             const float e1 = plane(1, l1 + size);
             const float e2 = plane(2, l2 + size);
@@ -454,7 +620,10 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             l1 = n1 & ~(size - 1u);
             l2 = n2 & ~(size - 1u);
             // m == 1: the ancestor is the node we are iterating (still in `node`)
-            if (m > 1) node = depth ? stk[(depth - 1 - sb) * kBlockThreads] : S.root;
+            if (m > 1) {
+                RT_BS(kBsPop);
+                node = depth ? stk[(depth - 1 - sb) * kBlockThreads] : S.root;
+            }
             t = texit;
         }
     }
@@ -781,6 +950,59 @@ __device__ __forceinline__ PixelOut sample_color(const FrameArgs& a, uint32_t x,
 }
 #endif  // RT_AB_VARIANTS (separate primary/shadow walks)
 
+// The bundle of the rays `active` lanes are about to walk (converged code:
+// every lane of the wave executes this).  Reference = the first active lane's
+// ray; A, B = the largest origin / direction distance from it.
+__device__ __forceinline__ void make_bundle(Bundle& bn, bool active, float o0, float o1, float o2,
+                                            float d0, float d1, float d2) {
+    const uint64_t am = __ballot(active);
+    bn.ok = false;
+    if (am == 0) return;
+    const uint32_t f = static_cast<uint32_t>(__builtin_ctzll(am));
+    bn.o0 = readlane_f(o0, f);
+    bn.o1 = readlane_f(o1, f);
+    bn.o2 = readlane_f(o2, f);
+    bn.d0 = readlane_f(d0, f);
+    bn.d1 = readlane_f(d1, f);
+    bn.d2 = readlane_f(d2, f);
+    float ea = 0.0f, eb = 0.0f;
+    if (active) {
+        const float x = o0 - bn.o0, y = o1 - bn.o1, z = o2 - bn.o2;
+        const float u = d0 - bn.d0, v = d1 - bn.d1, w = d2 - bn.d2;
+        ea = fmaf(z, z, fmaf(y, y, x * x));
+        eb = fmaf(w, w, fmaf(v, v, u * u));
+    }
+    // a non-finite lane (or reference) disables the prefilter for the walk
+    const bool bad = active && !(ea <= 3.0e38f && eb <= 3.0e38f &&
+                                 fabsf(o0) <= 3.0e38f && fabsf(o1) <= 3.0e38f && fabsf(o2) <= 3.0e38f);
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) {
+        ea = fmaxf(ea, __shfl_xor(ea, m, 64));
+        eb = fmaxf(eb, __shfl_xor(eb, m, 64));
+    }
+    if (__any(bad)) return;
+    // every lane holds the maxima now: make them wave-uniform (SGPRs)
+    const float A = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(sqrtf(ea))));
+    const float B = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(sqrtf(eb))));
+    if (!(B <= 0.5f) || !(A <= 1.0e30f)) return;
+    bn.c0 = fmaf(kBundleEps, 1.0f + A, A + A * B);
+    bn.c1 = kBundleEps + B;
+    bn.c2 = 1.0f + 2.0f * B;
+    bn.ok = true;
+}
+
+// The kernel's FrameArgs as memory (the kernarg segment, scalar-cached),
+// behind an opaque pointer: a field read through it is a fresh s_load at that
+// point instead of a value kept live in an SGPR across the walk (the register
+// allocator would spill it into VGPR lanes: v_writelane / v_readlane, VALU
+// work per pixel).  Used for the per-sample camera, shading and output fields.
+typedef __attribute__((address_space(4))) const FrameArgs KernArgs;
+__device__ __forceinline__ KernArgs* kernargs() {
+    KernArgs* p = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
 // Unified lane path: one walk instance run twice (primary, then the shadow ray
 // of the lanes that need one), so the register allocator sees one walk.
 // kLeafMode: 0 vector loads, 1 LDS-staged uniform leaves, 2 scalar-loaded uniform
@@ -790,16 +1012,22 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
                                                          uint32_t y, uint32_t hp, uint32_t s,
                                                          bool valid, uint32_t& n_shadow,
                                                          uint32_t& n_nodes, uint32_t& n_prims,
-                                                         void* stk, float4* lbuf = nullptr) {
+                                                         void* stk, float4* lbuf = nullptr,
+                                                         uint32_t* bs = nullptr) {
     const SceneArgs& S = a.sc;
+    KernArgs* ka = kernargs();
     float u = static_cast<float>(x), v = static_cast<float>(y);
-    if (a.jitter) {
+    if (ka->jitter) {
         u = u + u01(mix32(hp ^ (s << 1)));
         v = v + u01(mix32(hp ^ ((s << 1) | 1u)));
     }
-    float r0 = a.cam.o[0], r1 = a.cam.o[1], r2 = a.cam.o[2];
+    float r0 = ka->cam.o[0], r1 = ka->cam.o[1], r2 = ka->cam.o[2];
     float d0, d1, d2;
-    get_ray(a.cam, u, v, d0, d1, d2);
+    {
+        CamArgs cam;
+        for (int i = 0; i < 9; ++i) cam.K[i] = ka->cam.K[i], cam.R[i] = ka->cam.R[i];
+        get_ray(cam, u, v, d0, d1, d2);
+    }
     const float miss_g = sat(d1), miss_b = sat(d2);
     bool active = valid, any = false, hit0 = false;
     float lam = 0.0f;
@@ -808,16 +1036,21 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
         float t = 0.0f;
         uint32_t idx = 0;
         bool hit = false;
-        if (active)
+        Bundle bun;
+        if (kLeafMode == 4) make_bundle(bun, active, r0, r1, r2, d0, d1, d2);
+        if (active) {
+            RT_BS(kBsPhase);
             hit = walk<false, kChunk, true, kStats, kLeafMode == 1, kLeafMode == 2,
-                       kLeafMode == 3>(
+                       kLeafMode == 3, kLeafMode == 4>(
                 S, r0, r1, r2, d0, d1, d2, 0.0f, INFINITY, t, idx, n_nodes, n_prims,
-                static_cast<uint2*>(stk), any, lbuf);
+                static_cast<uint2*>(stk), any, lbuf, bs, &bun);
+        }
         if (phase == 0) {
             hit0 = active && hit;
             bool want_shadow = false;
+            KernArgs* kb = kernargs();
             if (hit0) {
-                const float4 sp = S.spheres[idx];
+                const float4 sp = kb->sc.spheres[idx];
                 const float p0 = r0 + t * d0;
                 const float p1 = r1 + t * d1;
                 const float p2 = r2 + t * d2;
@@ -825,16 +1058,16 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
                 const float n0 = (p0 - sp.x) * ir;
                 const float n1 = (p1 - sp.y) * ir;
                 const float n2 = (p2 - sp.z) * ir;
-                const float ndl = n0 * a.L[0] + n1 * a.L[1] + n2 * a.L[2];
+                const float ndl = n0 * kb->L[0] + n1 * kb->L[1] + n2 * kb->L[2];
                 lam = ndl > 0.0f ? ndl : 0.0f;
-                want_shadow = ndl > 0.0f && a.shadows;
-                al = S.albedo[idx];
+                want_shadow = ndl > 0.0f && kb->shadows;
+                al = kb->sc.albedo[idx];
                 r0 = p0 + n0 * kShadowEps;
                 r1 = p1 + n1 * kShadowEps;
                 r2 = p2 + n2 * kShadowEps;
-                d0 = a.L[0];
-                d1 = a.L[1];
-                d2 = a.L[2];
+                d0 = kb->L[0];
+                d1 = kb->L[1];
+                d2 = kb->L[2];
             }
             active = want_shadow;
             any = true;
@@ -846,7 +1079,8 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
     }
     PixelOut c{200.0f / 255.0f, miss_g, miss_b};
     if (hit0) {
-        const float f = a.ambient + (1.0f - a.ambient) * lam;
+        const float amb = kernargs()->ambient;
+        const float f = amb + (1.0f - amb) * lam;
         c.r = static_cast<float>(al & 0xFFu) * (1.0f / 255.0f) * f;
         c.g = static_cast<float>((al >> 8) & 0xFFu) * (1.0f / 255.0f) * f;
         c.b = static_cast<float>((al >> 16) & 0xFFu) * (1.0f / 255.0f) * f;
@@ -864,7 +1098,7 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
                                                 uint32_t ox, uint32_t oy, uint32_t k,
                                                 uint32_t olx, uint32_t oly, uint32_t& n_primary,
                                                 uint32_t& n_shadow, uint32_t& n_nodes,
-                                                uint32_t& n_prims) {
+                                                uint32_t& n_prims, uint32_t* bs = nullptr) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t spw = a.spw, g = a.g;
     const uint32_t pix = lane / g, sub = lane & (g - 1u);
@@ -889,13 +1123,13 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
 #ifdef RT_AB_VARIANTS
         PixelOut c = kVar == kVariantLaneUnified
                          ? sample_color_unified<kChunk, kStats, kLeafMode>(
-                               a, x, y, hp, sg, valid, n_shadow, n_nodes, n_prims, stk, lbuf)
+                               a, x, y, hp, sg, valid, n_shadow, n_nodes, n_prims, stk, lbuf, bs)
                          : sample_color<kVar, kChunk>(a, x, y, hp, sg, valid, n_shadow,
                                                             n_nodes, n_prims, stk);
 #else
         static_assert(kVar == kVariantLaneUnified, "other walks are A/B builds (-DRT_AB_VARIANTS)");
         PixelOut c = sample_color_unified<kChunk, kStats, kLeafMode>(
-            a, x, y, hp, sg, valid, n_shadow, n_nodes, n_prims, stk, lbuf);
+            a, x, y, hp, sg, valid, n_shadow, n_nodes, n_prims, stk, lbuf, bs);
 #endif
         // Pixel sum of this round: pairwise butterfly over the pixel's g
         // lanes (missing samples are 0) = oracle.c:tree_sum; rounds are then
@@ -916,20 +1150,24 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
             acc[threadIdx.x] = make_float4(c.r, c.g, c.b, 0.0f);
         }
     }
+    // outputs: fields read afresh (kernargs()), not kept live across the walks
+    KernArgs* ko = kernargs();
     if (leader) {
         const float4 A = acc[threadIdx.x];
-        if (kProg) a.accum[(size_t)y * a.W + x] = A;
-        const PixelOut p{A.x * a.inv_spp, A.y * a.inv_spp, A.z * a.inv_spp};
+        if (kProg) ko->accum[(size_t)y * ko->W + x] = A;
+        const float isp = ko->inv_spp;
+        const PixelOut p{A.x * isp, A.y * isp, A.z * isp};
         const uint32_t rgba = pack_rgba8(p);
         if (kTiles) {
-            a.out8[(size_t)k * a.tile_size * a.tile_size + (oly + qy) * a.tile_size + olx + qx] = rgba;
+            const uint32_t ts = ko->tile_size;
+            ko->out8[(size_t)k * ts * ts + (oly + qy) * ts + olx + qx] = rgba;
         } else {
-            a.out8[(size_t)y * a.W + x] = rgba;
-            if (a.out32) a.out32[(size_t)y * a.W + x] = make_float4(p.r, p.g, p.b, 1.0f);
+            ko->out8[(size_t)y * ko->W + x] = rgba;
+            if (ko->out32) ko->out32[(size_t)y * ko->W + x] = make_float4(p.r, p.g, p.b, 1.0f);
         }
-    } else if (kTiles && sub == 0 && pix < a.ppw) {
-        a.out8[(size_t)k * a.tile_size * a.tile_size + (oly + qy) * a.tile_size + olx + qx] =
-            0u;  // off-image pixel of an edge tile
+    } else if (kTiles && sub == 0 && pix < ko->ppw) {
+        const uint32_t ts = ko->tile_size;
+        ko->out8[(size_t)k * ts * ts + (oly + qy) * ts + olx + qx] = 0u;  // off-image pixel of an edge tile
     }
 }
 
@@ -968,6 +1206,11 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
     }
     const uint32_t tw = a.tw, th = a.th;
     uint32_t n_shadow = 0, n_nodes = 0, n_prims = 0, n_primary = 0;
+#ifdef RT_BLOCK_STATS
+    uint32_t bs[2 * kBlockStats] = {};
+#else
+    uint32_t* bs = nullptr;
+#endif
 #ifdef RT_TIMELINE
     // diagnostic build only (tools/timeline.sh): per-wave {start, first empty
     // range, exit, units} in wall-clock ticks
@@ -1025,7 +1268,7 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
                 const unsigned long long tu0 = wall_clock64();
 #endif
                 shade_wave_tile<kTiles, kVar, kChunk, kStats, kProg, kLeafMode>(
-                    a, acc, stk, lbuf, ox, oy, k, olx, oly, n_primary, n_shadow, n_nodes, n_prims);
+                    a, acc, stk, lbuf, ox, oy, k, olx, oly, n_primary, n_shadow, n_nodes, n_prims, bs);
 #ifdef RT_TIMELINE
                 // per unit {start, end} after the 65536 per-wave records
                 const unsigned long long uid = (unsigned long long)sb * 4096u + (cur & 4095u);
@@ -1068,11 +1311,20 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
                 const uint32_t wox = (wt % wtx) * tw, woy = (wt / wtx) * th;
                 shade_wave_tile<kTiles, kVar, kChunk, kStats, kProg, kLeafMode>(
                     a, acc, stk, lbuf, ox + wox, oy + woy, k, olx + wox, oly + woy, n_primary,
-                    n_shadow, n_nodes, n_prims);
+                    n_shadow, n_nodes, n_prims, bs);
             }
         }
     }
     flush_counters(a, n_primary, n_shadow, n_nodes, n_prims);
+#ifdef RT_BLOCK_STATS
+    if (a.bstats) {
+#pragma unroll
+        for (uint32_t i = 0; i < 2 * kBlockStats; ++i) {
+            const unsigned long long v = wave_sum(bs[i]);
+            if ((threadIdx.x & 63u) == 0) atomicAdd(a.bstats + i, v);
+        }
+    }
+#endif
 #ifdef RT_TIMELINE
     tl_units = n_primary / 64u;  // samples cast by the wave / 64
     if (a.timeline && (threadIdx.x & 63u) == 0) {
@@ -1264,6 +1516,14 @@ static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStr
             break;
 #ifdef RT_AB_VARIANTS
         // measured-and-rejected alternatives, A/B builds only
+        case kVariantWaveQBundle:  // 13 + bundle-prefiltered leaves
+            if (a.count_work)
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, true, false, true, 4>,
+                             a, lds, st);
+            else
+                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, false, false, true, 4>,
+                             a, lds, st);
+            break;
         case kVariantPacket:
             launch_persistent(scene_kernel<kTiles, kVariantPacket, 1, 4>, a, n_bt, lds, st);
             break;
@@ -1326,7 +1586,7 @@ bool variant_available(uint32_t v) {
 #ifdef RT_AB_VARIANTS
     return v == kVariantLane || v == kVariantPacket || v == kVariantLaneChunk2 ||
            v == kVariantWaveQLds || v == kVariantWaveQSmem || v == kVariantWaveQLane ||
-           v == kVariantWaveQ6 || v == kVariantWaveQ8;
+           v == kVariantWaveQ6 || v == kVariantWaveQ8 || v == kVariantWaveQBundle;
 #else
     return false;
 #endif

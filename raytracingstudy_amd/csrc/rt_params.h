@@ -28,6 +28,7 @@ constexpr uint32_t kVariantWaveQSmem = 15; // 13 + wave-uniform leaves read by s
 constexpr uint32_t kVariantWaveQLane = 12; // 13 + one-lane leaf loads, readfirstlane broadcast
 constexpr uint32_t kVariantWaveQ6 = 8;     // 13 at 6 waves/SIMD, no spills (A/B)
 constexpr uint32_t kVariantWaveQ8 = 9;     // 13 compiled for 8 waves/SIMD (A/B)
+constexpr uint32_t kVariantWaveQBundle = 11;  // 13 + bundle-prefiltered leaves (A/B)
 constexpr uint32_t kPrimPad = 4;           // prim_sp padding: scalar reads may run 3 past a leaf
 
 // A/B toggles (rt_config.flags bits 20..27), results identical either way
@@ -57,6 +58,28 @@ constexpr uint32_t kQueueSlot = 8;
 constexpr uint32_t kWaveQueueBase = 16;
 constexpr uint32_t kWaveQueueStride = 16;
 constexpr uint32_t kCounterWords = kWaveQueueBase + 8 * kWaveQueueStride;
+
+// Diagnostic build (-DRT_BLOCK_STATS, tools/block_stats.py): how many times a
+// wave executed each block of the walk (a block runs once for the wave when
+// any lane is in it), and how many lanes were active.  [2*i] = executions of
+// block i, [2*i+1] = active lanes summed over those executions.
+enum BlockStat : uint32_t {
+    kBsIter = 0,      // walk loop trips
+    kBsJump,          // trips taking the cell-table jump path
+    kBsJumpDescend,   // mid-plane steps inside a jump (while depth < K)
+    kBsDescend,       // trips taking the record-descent path
+    kBsInternal,      // descents into an internal child (continue)
+    kBsLeaf,          // leaves entered
+    kBsLeafChunk,     // leaf chunk trips (kChunk spheres each)
+    kBsTest,          // sphere tests (one per slot of a chunk)
+    kBsSqrt,          // tests past h >= 0 (square root path)
+    kBsAccept,        // tests returning a hit
+    kBsExit,          // exit-plane steps
+    kBsPop,           // pops reading the LDS stack (m > 1)
+    kBsWalk,          // walks started (root box entered)
+    kBsPhase,         // sample phases (primary / shadow) run by the wave
+    kBlockStats
+};
 
 // Wave mapping of the scene kernel: spw = min(spp, 64) samples of a pixel on
 // g = pow2ceil(spw) lanes, ppw = 64 / g pixels per wave as a tw x th tile.
@@ -137,6 +160,9 @@ struct FrameArgs {
     uint32_t wq_chunk;    // wave-queue scheduling: wave tiles per dequeue ticket (launch_scene)
 #ifdef RT_TIMELINE
     unsigned long long* timeline;  // diagnostic build: 4 words per wave
+#endif
+#ifdef RT_BLOCK_STATS
+    unsigned long long* bstats;    // diagnostic build: kBlockStats wave-execution counters
 #endif
 };
 

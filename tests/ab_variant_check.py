@@ -22,7 +22,7 @@ import oracle  # noqa: E402
 import raytracingstudy_amd as rt  # noqa: E402
 from raytracingstudy_amd.camera import scene_pose  # noqa: E402
 
-AB_VARIANTS = [1, 2, 3, 8, 9, 12, 14, 15]
+AB_VARIANTS = [1, 2, 3, 8, 9, 11, 12, 14, 15]
 CASES = [  # n, w, h, spp, depth
     (1000, 160, 120, 1, 7),
     (20000, 128, 96, 2, 12),

@@ -32,4 +32,4 @@ def test_ab_variants_match_oracle(gpu):
                        env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
     res = json.loads(p.stdout.strip().splitlines()[-1])
-    assert res["ok"] and len(res["cases"]) == 32
+    assert res["ok"] and len(res["cases"]) == 36
