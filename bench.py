@@ -30,6 +30,10 @@ NODE_BYTES = 8     # uint2 node record
 PRIM_BYTES = 16    # float4 sphere record per ray-sphere test
 PIXEL_BYTES = 4    # RGBA8 framebuffer write
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# scalar pipeline (SALU + branch instructions) per CU: one per cycle
+# (MI355X_MICROARCH.md: 1 scalar unit per CU; measured 0.99 SALU and 1.07
+# SALU+branch per CU-cycle by tools/scalar_peak.hip, profiles/r02/scalar_peak.json)
+SCALAR_PER_CU_CYCLE = 1.0
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s over the 8 XCDs
 
 
@@ -121,6 +125,9 @@ def roofline(kern_ms: float, touched_bytes: float, pmc, simds: int, pmc_path: st
              pmc_note: str = "") -> dict:
     """Every roof this kernel could sit under, each computed from measured data,
     and the binding one (largest valid fraction) on top:
+      * scalar_issue: PMC SQ_INSTS_SALU + SQ_INSTS_BRANCH per launch over the
+        live kernel time, against one scalar instruction per CU-cycle (the
+        CU's single scalar unit; the divergent walk's exec-mask bookkeeping);
       * valu_issue: PMC SQ_INSTS_VALU per launch over the live kernel time,
         against SIMDs x clock / 2 (a wave64 VALU instruction occupies a
         SIMD-32 for 2 cycles, MI355X_MICROARCH.md "Wave scheduling");
@@ -147,6 +154,18 @@ def roofline(kern_ms: float, touched_bytes: float, pmc, simds: int, pmc_path: st
                                    "unit": "G wave-instr/s", "frac": round(rate / peak, 4),
                                    "insts_per_launch": insts, "clock_ghz": round(clock, 4),
                                    "simds": simds, "source": src + ": SQ_INSTS_VALU, GRBM_GUI_ACTIVE"}
+        sq = pmc.get("sq", {})
+        if sq.get("SQ_INSTS_SALU") and clock:
+            # one CU = 4 SIMDs
+            sc = sq["SQ_INSTS_SALU"] + sq.get("SQ_INSTS_BRANCH", 0.0)
+            peak = simds / 4 * clock * 1e9 * SCALAR_PER_CU_CYCLE
+            rate = sc / secs
+            roofs["scalar_issue"] = {"achieved": round(rate / 1e9, 2), "peak": round(peak / 1e9, 2),
+                                     "unit": "G instr/s", "frac": round(rate / peak, 4),
+                                     "salu_per_launch": sq["SQ_INSTS_SALU"],
+                                     "branch_per_launch": sq.get("SQ_INSTS_BRANCH"),
+                                     "source": src + ": SQ_INSTS_SALU + SQ_INSTS_BRANCH vs 1 per "
+                                                     "CU-cycle (tools/scalar_peak.hip)"}
         if traffic:
             rate = traffic / secs / 1e9
             roofs["hbm"] = {"achieved": round(rate, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -505,10 +505,16 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         const uint32_t sb = K ? K - 1u : 0u;
         // Hard cap (never reached by a correct walk: a ray crosses < 3*G cells
         // and each crossing costs at most one descent): no input can hang the GPU.
+        // One exit per trip (`stop`): the any-hit, nearest-done, ray-left and
+        // root-left conditions are OR-ed into one flag, so the wave's exec
+        // bookkeeping is one loop-exit mask update per trip (the scalar pipe is
+        // this kernel's busiest unit, profiles/r02/pmc_sq_screen.json).
+        bool any_hit = false;
         for (uint32_t it = 0, cap = 8u * G + 64u; it < cap; ++it) {
             RT_BS(kBsIter);
-            uint2 rec;
-            bool have;  // rec is a leaf record (else the cell is empty)
+            uint2 rec = make_uint2(0u, 0u);
+            bool have = false;   // rec is a leaf record (else the cell is empty)
+            bool inner = false;  // stepped into an internal node: descend next trip
             if (jump) {
                 RT_BS(kBsJump);
                 jump = false;
@@ -539,11 +545,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 // the oracle reads one record per level from `from` down to
                 // the covering node (an empty child's own level reads none)
                 if (kStats) n_nodes += (kind == kCellEmpty ? depth - 1u : depth) - from;
-                if (kind == kCellInternal) {
-                    node = rec;
-                    stk[(depth - 1 - sb) * kBlockThreads] = rec;
-                    continue;
-                }
+                inner = kind == kCellInternal;
                 have = kind == kCellLeaf;
             } else {
                 RT_BS(kBsDescend);
@@ -564,17 +566,17 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                     const uint32_t slot = node.x + __builtin_popcount(valid & ((1u << child) - 1u));
                     rec = nodes[slot];
                     if (kStats) n_nodes += 1;
-                    if (!((node.y >> 8) & (1u << child))) {
-                        RT_BS(kBsInternal);
-                        node = rec;
-                        stk[(depth - 1 - sb) * kBlockThreads] = rec;
-                        continue;
-                    }
+                    inner = !((node.y >> 8) & (1u << child));
+                    have = !inner;
                 }
             }
-            if (have) {
-                if (leaf(rec.x, rec.y)) return true;
+            if (inner) {
+                RT_BS(kBsInternal);
+                node = rec;
+                stk[(depth - 1 - sb) * kBlockThreads] = rec;
+                continue;
             }
+            if (have) any_hit = leaf(rec.x, rec.y);
             RT_BS(kBsExit);
             const float e0 = plane(0, l0 + size);
             const float e1 = plane(1, l1 + size);
@@ -582,16 +584,20 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             // one v_min3_f32 (the oracle's ternaries can differ only in the sign
             // of a zero, and texit is only ever compared: identical walks)
             const float texit = fminf(fminf(e0, e1), e2);
-            if (!kAnyHit && best_t < texit) break;
-            if (texit >= t1) break;
             // step every axis whose exit plane is texit; the flipped bits give the
             // common ancestor (oracle.c: diff of the cell coordinates)
             const uint32_t n0 = e0 == texit ? l0 + size : l0;
             const uint32_t n1 = e1 == texit ? l1 + size : l1;
             const uint32_t n2 = e2 == texit ? l2 + size : l2;
-            if ((n0 | n1 | n2) >= G) break;  // left the root
+            // leave on an any-hit, a nearest hit before this cell's exit, the
+            // ray's end, or the root's boundary (the same order of tests as
+            // the oracle, whose results do not depend on that order)
+            const bool stop = any_hit | (!kAnyHit & (best_t < texit)) | (texit >= t1) |
+                              ((n0 | n1 | n2) >= G);
+            if (stop) break;
             const uint32_t diff = (l0 ^ n0) | (l1 ^ n1) | (l2 ^ n2);
             const uint32_t top = 31u - __builtin_clz(diff);  // highest flipped bit
+            t = texit;
             if (D - (top + 1u) < K) {
                 // the common ancestor lies above the table level: jump.  A cell
                 // at depth >= K indexes the table directly from its corner; a
@@ -609,23 +615,22 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 }
                 if (kStats) from = D - (top + 1u);
                 jump = true;
-                t = texit;
-                continue;
+            } else {
+                // ancestor cell size = 2^(top+1); its depth = D - (top+1)
+                size = 2u << top;
+                const uint32_t m = depth - (D - (top + 1u));
+                depth -= m;
+                l0 = n0 & ~(size - 1u);
+                l1 = n1 & ~(size - 1u);
+                l2 = n2 & ~(size - 1u);
+                // m == 1: the ancestor is the node we are iterating (still in `node`)
+                if (m > 1) {
+                    RT_BS(kBsPop);
+                    node = depth ? stk[(depth - 1 - sb) * kBlockThreads] : S.root;
+                }
             }
-            // ancestor cell size = 2^(top+1); its depth = D - (top+1)
-            size = 2u << top;
-            const uint32_t m = depth - (D - (top + 1u));
-            depth -= m;
-            l0 = n0 & ~(size - 1u);
-            l1 = n1 & ~(size - 1u);
-            l2 = n2 & ~(size - 1u);
-            // m == 1: the ancestor is the node we are iterating (still in `node`)
-            if (m > 1) {
-                RT_BS(kBsPop);
-                node = depth ? stk[(depth - 1 - sb) * kBlockThreads] : S.root;
-            }
-            t = texit;
         }
+        if (any_hit) return true;
     }
     if (!kAnyHit && best_ref != kNoHit) {
         tout = best_t;

@@ -28,7 +28,8 @@ def test_valu_issue_is_the_bound_when_hbm_traffic_is_tiny():
     r = bench.roofline(kern_ms, touched, pmc, SIMDS)
     assert r["frac"] is not None and 0 < r["frac"] <= 1.0
     assert r["traffic"] / touched < 0.01
-    assert r["bound"] != "hbm" and r["bound"] == "valu_issue"
+    # the issue roofs bind (scalar pipe or VALU), never HBM
+    assert r["bound"] in ("scalar_issue", "valu_issue")
     v = r["roofs"]["valu_issue"]
     insts = pmc["sq"]["SQ_INSTS_VALU"]
     peak = SIMDS * pmc["effective_clock_ghz"] / 2.0  # G wave-instructions / s
@@ -61,3 +62,17 @@ def test_stale_pmc_summary_is_refused(tmp_path):
     ent, why = bench.load_pmc(str(p), pmc["config"], 1, kernel_source_id())
     assert ent is not None and why == "ok"
     assert bench.load_pmc(str(p), "c5", 1, kernel_source_id())[0] is None
+
+
+def test_scalar_issue_roof_when_counted():
+    pmc = dict(_pmc())
+    sq = dict(pmc["sq"], SQ_INSTS_SALU=4.81e9, SQ_INSTS_BRANCH=1.13e9)
+    pmc["sq"] = sq
+    kern_ms = 11.65
+    r = bench.roofline(kern_ms, 182e9, pmc, SIMDS)
+    s = r["roofs"]["scalar_issue"]
+    peak = SIMDS / 4 * pmc["effective_clock_ghz"]  # G instr/s
+    assert s["frac"] == pytest.approx((4.81 + 1.13) / (kern_ms / 1e3) / peak, rel=1e-3)
+    # the binding roof is the largest valid fraction
+    valid = {k: v["frac"] for k, v in r["roofs"].items() if v["frac"] <= 1}
+    assert r["bound"] == max(valid, key=valid.get)

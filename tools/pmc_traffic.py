@@ -95,6 +95,10 @@ def main():
             res["effective_clock_ghz"] = gui / 8.0 / _median(durs)
         if waves:
             res["valu_insts_per_wave"] = sq.get("SQ_INSTS_VALU", (0, 0))[0] / waves
+        if gui and sq.get("SQ_INSTS_SALU"):
+            # per CU-cycle (256 CUs, GRBM_GUI_ACTIVE summed over 8 XCDs)
+            sc = sq["SQ_INSTS_SALU"][0] + sq.get("SQ_INSTS_BRANCH", (0, 0))[0]
+            res["scalar_per_cu_cycle"] = sc / 256.0 / (gui / 8.0)
     print(json.dumps(res, indent=1))
 
 
