@@ -447,7 +447,10 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         const float4* __restrict__ ps = prim_sp + off;
         static_assert(kChunk <= kPrimPad + 1, "leaf loads may run kChunk-1 spheres past a leaf");
         RT_BS(kBsLeaf);
-        for (uint32_t j = 0; j < cnt; j += kChunk) {
+        // cnt >= 1 (a leaf is a non-empty cell; the root leaf is guarded by
+        // its caller): a do-while skips the loop-entry test and its branch
+        uint32_t j = 0;
+        do {
             RT_BS(kBsLeafChunk);
             const uint32_t m = cnt - j;
             // kChunk unconditional dwordx4 loads in flight at fixed offsets; a
@@ -474,19 +477,20 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 const bool pos = !(isect_h(o0, o1, o2, d0, d1, d2, sv[q]) < 0.0f);
                 maybe |= (m > static_cast<uint32_t>(q)) & pos;
             }
-            if (!__any(maybe)) {
-                if (kStats) n_prims += min(m, static_cast<uint32_t>(kChunk));
-                continue;
-            }
+            if (__any(maybe)) {
 #pragma unroll
-            for (int q = 0; q < kChunk; ++q)
-                if (m > static_cast<uint32_t>(q) && test(sv[q], off + j + q)) return true;
-        }
+                for (int q = 0; q < kChunk; ++q)
+                    if (m > static_cast<uint32_t>(q) && test(sv[q], off + j + q)) return true;
+            } else if (kStats) {
+                n_prims += min(m, static_cast<uint32_t>(kChunk));
+            }
+            j += kChunk;
+        } while (j < cnt);
         return false;
     };
 
     if (S.root_is_leaf) {
-        if (leaf(S.root.x, S.root.y)) return true;
+        if (S.root.y && leaf(S.root.x, S.root.y)) return true;  // an empty scene's root holds 0
     } else {
         uint2 node = S.root;
         // Cell = (depth, lower corner l* in finest-grid units, size = G >> depth):
@@ -598,36 +602,30 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             const uint32_t diff = (l0 ^ n0) | (l1 ^ n1) | (l2 ^ n2);
             const uint32_t top = 31u - __builtin_clz(diff);  // highest flipped bit
             t = texit;
-            if (D - (top + 1u) < K) {
-                // the common ancestor lies above the table level: jump.  A cell
-                // at depth >= K indexes the table directly from its corner; a
-                // shallower one resolves down to K from the ancestor's cell.
-                if (depth < K) {
-                    size = 2u << top;
-                    depth = D - (top + 1u);
-                    l0 = n0 & ~(size - 1u);
-                    l1 = n1 & ~(size - 1u);
-                    l2 = n2 & ~(size - 1u);
-                } else {
-                    l0 = n0;
-                    l1 = n1;
-                    l2 = n2;
-                }
-                if (kStats) from = D - (top + 1u);
-                jump = true;
-            } else {
-                // ancestor cell size = 2^(top+1); its depth = D - (top+1)
-                size = 2u << top;
-                const uint32_t m = depth - (D - (top + 1u));
-                depth -= m;
-                l0 = n0 & ~(size - 1u);
-                l1 = n1 & ~(size - 1u);
-                l2 = n2 & ~(size - 1u);
-                // m == 1: the ancestor is the node we are iterating (still in `node`)
-                if (m > 1) {
-                    RT_BS(kBsPop);
-                    node = depth ? stk[(depth - 1 - sb) * kBlockThreads] : S.root;
-                }
+            // The common ancestor: size 2^(top+1), depth D - (top+1).  Above the
+            // table level the walk jumps: a cell at depth >= K indexes the table
+            // straight from the neighbour's corner (`keep`), a shallower one
+            // resolves down to K from the ancestor's cell.  Otherwise it pops
+            // to the ancestor.  Selects, not branches: every lane ends the trip
+            // with the same instructions (the scalar pipe carries the branches'
+            // exec-mask updates, and it is the kernel's busiest unit).
+            const uint32_t adepth = D - (top + 1u);
+            const bool above = adepth < K;
+            const bool keep = above && depth >= K;
+            const uint32_t asize = 2u << top;
+            const uint32_t m = depth - adepth;  // levels popped (when !above)
+            const uint32_t am = keep ? 0xFFFFFFFFu : ~(asize - 1u);
+            l0 = n0 & am;
+            l1 = n1 & am;
+            l2 = n2 & am;
+            size = keep ? size : asize;
+            depth = keep ? depth : adepth;
+            if (kStats && above) from = adepth;
+            jump = above;
+            // m == 1: the ancestor is the node we are iterating (still in `node`)
+            if (!above && m > 1) {
+                RT_BS(kBsPop);
+                node = depth ? stk[(depth - 1 - sb) * kBlockThreads] : S.root;
             }
         }
         if (any_hit) return true;
