@@ -58,7 +58,7 @@ def parse():
                          "the multi-rank path on one GPU)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal: every rank uses cuda:0 (with --backend gloo)")
-    ap.add_argument("--secondary", default="c2,c5",
+    ap.add_argument("--secondary", default="c2,c5,c5d",
                     help="N=1 only: also time these configs (a few frames each) and report them "
                          "under `secondary`; '' to skip")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
@@ -73,7 +73,7 @@ def cpu_baseline(cfg, K, pose, target_s: float) -> dict:
     import oracle
     import raytracingstudy_amd as rt
 
-    sp, al = rt.generate_spheres(cfg.n_spheres, rt.SEED)
+    sp, al = rt.configs.scene_spheres(cfg, rt.SEED)
     sc = oracle.Scene(sp, al, max_depth=cfg.max_depth)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or oracle.max_threads()
     # calibrate on one row, then take every step-th row for ~target_s seconds
@@ -195,7 +195,7 @@ def secondary_config(rt, torch, name: str, dev, stream, steps: int = 3) -> dict:
     from raytracingstudy_amd.camera import scene_pose
 
     c = rt.CONFIGS[name]
-    sp, al = rt.generate_spheres(c.n_spheres, rt.SEED)
+    sp, al = rt.configs.scene_spheres(c, rt.SEED)
     r2 = rt.KernelRenderer(c.width, c.height, mode="scene", spp=c.spp, device=dev.index)
     try:
         r2.resize(c.width, c.height)
@@ -213,8 +213,9 @@ def secondary_config(rt, torch, name: str, dev, stream, steps: int = 3) -> dict:
             e1.synchronize()
             ms.append(e0.elapsed_time(e1))
         k = float(np.median(ms))
-        return {"workload": f"{c.width}x{c.height}, {c.spp} spp, {c.n_spheres} spheres, "
-                            f"depth {info['max_depth']}",
+        return {"workload": f"{c.width}x{c.height}, {c.spp} spp, {c.n_spheres} {c.scene} spheres, "
+                            f"max depth {info['max_depth']}",
+                "depth_reached": info["depth_reached"], "cell_table_depth": info["cell_table_depth"],
                 "kernel_ms": round(k, 3), "Mrays_s": round(rays / k / 1e3, 1),
                 "rays_per_frame": int(rays), "scene_build_ms": round(info["build_ms"], 2),
                 "octree_nodes": info["n_nodes"], "prim_refs": info["n_prim_refs"]}
@@ -250,7 +251,7 @@ def main():
     if cfg.mode != "scene":
         raise SystemExit("bench runs a scene config (c2..c5)")
 
-    sp, al = rt.generate_spheres(cfg.n_spheres, rt.SEED)
+    sp, al = rt.configs.scene_spheres(cfg, rt.SEED)
     r = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=cfg.spp, device=local,
                           light_dir=rt.configs.LIGHT_DIR, ambient=rt.configs.AMBIENT,
                           variant=args.variant)

@@ -82,6 +82,9 @@ enum {
     RT_FLAG_PROGRESSIVE = 1u << 5, /* scene mode: accumulate samples across frames while the
                                       camera, size, scene and tile list stay unchanged; every
                                       frame adds spp samples */
+    RT_FLAG_COMPAT_FMA = 1u << 6,  /* compat mode: evaluate getRay (include/camera.h:31-34) with
+                                      the FMA contraction nvcc's default -fmad=true applies to
+                                      the reference binary; off = source order */
     /* bits 16..19: scene-kernel variant for A/B runs (0 = default: 13, the
      * per-wave queue, for spp >= 8, else 7; others in DESIGN.md 5.1); images
      * and counters are identical across variants (packets: images only) */

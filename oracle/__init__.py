@@ -37,6 +37,7 @@ def load() -> ctypes.CDLL:
         "orc_get_ray": (None, [_P, _P, _f, _f, _P]),
         "orc_hit_root_box": (ctypes.c_int, [_P, _P]),
         "orc_render_compat": (None, [_u32, _u32, _P, _P, _P]),
+        "orc_render_compat_fma": (None, [_u32, _u32, _P, _P, ctypes.c_int, _P]),
         "orc_generate_spheres": (None, [_u32, _u32, _P, _P]),
         "orc_sample_hash": (_u32, [_u32, _u32, _u32, _u32]),
         "orc_scene_build": (_P, [_P, _P, _u32, _P, _P, _u32, _u32]),
@@ -83,6 +84,15 @@ def render_compat(w: int, h: int, pose, K) -> np.ndarray:
     out = np.zeros((h, w, 4), np.uint8)
     p, k = _f32(pose, 16), _f32(K, 9)  # keep the arrays alive across the call
     load().orc_render_compat(w, h, _p(p), _p(k), _p(out))
+    return out
+
+
+def render_compat_fma(w: int, h: int, pose, K, contract: int) -> np.ndarray:
+    """The compat image with getRay's sums FMA-contracted as nvcc would
+    (contract 1: NVVM operand order, 2: the other order, 0: none)."""
+    out = np.zeros((h, w, 4), np.uint8)
+    p, k = _f32(pose, 16), _f32(K, 9)
+    load().orc_render_compat_fma(w, h, _p(p), _p(k), int(contract), _p(out))
     return out
 
 

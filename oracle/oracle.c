@@ -61,6 +61,37 @@ void orc_get_ray(const float pose[16], const float K[9], float u, float v, float
     dir_out[2] = wdz;
 }
 
+/* include/camera.h:31-34 as nvcc would compile it with its default
+ * -fmad=true (the reference's CMakeLists.txt:2,16 sets no -fmad=false): the
+ * `a*b + c*d + e*1` sums contract into FMAs.  `rot[2][i] * dz` with the
+ * constant dz = 1 folds to rot[2][i] (x * 1.0 == x), and LLVM's DAG combiner
+ * (NVVM) fuses an fadd of two products through its FIRST operand:
+ *   contract = 1: wd = fmaf(rot[0][i], dx, rot[1][i] * dy) + rot[2][i]
+ *                 len = sqrtf(fmaf(wdz, wdz, fmaf(wdx, wdx, wdy * wdy)))
+ *   contract = 2: the other operand order (a bound on the ambiguity)
+ *                 wd = fmaf(rot[1][i], dy, rot[0][i] * dx) + rot[2][i]
+ *                 len = sqrtf(fmaf(wdz, wdz, fmaf(wdy, wdy, wdx * wdx)))
+ * contract = 0 is orc_get_ray (source order, no contraction).  Used to
+ * bound how far the reference BINARY can differ from its source semantics
+ * (tools/compat_fma_gap.py). */
+void orc_get_ray_fma(const float pose[16], const float K[9], float u, float v, int contract,
+                     float dir_out[3]) {
+    if (contract == 0) {
+        orc_get_ray(pose, K, u, v, dir_out);
+        return;
+    }
+    const float dx = (u - K[2]) / K[0];
+    const float dy = (v - K[5]) / K[4];
+    float w[3];
+    for (int i = 0; i < 3; ++i)
+        w[i] = contract == 1 ? fmaf(pose[i], dx, pose[4 + i] * dy) + pose[8 + i]
+                             : fmaf(pose[4 + i], dy, pose[i] * dx) + pose[8 + i];
+    const float l2 = contract == 1 ? fmaf(w[2], w[2], fmaf(w[0], w[0], w[1] * w[1]))
+                                   : fmaf(w[2], w[2], fmaf(w[1], w[1], w[0] * w[0]));
+    const float len = sqrtf(l2);
+    for (int i = 0; i < 3; ++i) dir_out[i] = w[i] / len;
+}
+
 /* src/renderer.cu:3-55.  Box min (0,0,0), max glm::vec3(1.28) (doubles -> f32),
  * centre glm::vec3(0.64) passed from :70.  Mixed f32/f64 exactly as written:
  * the mirrored origin is a float expression widened to double, the inverse is
@@ -92,15 +123,16 @@ int orc_hit_root_box(const float origin[3], const float dir[3]) {
 /* __saturatef: clamp to [0,1], NaN -> 0 */
 static inline float sat(float x) { return x > 0.0f ? (x < 1.0f ? x : 1.0f) : 0.0f; }
 
-/* src/renderer.cu:57-82.  Row-major uchar4, pid = y*W + x. */
-void orc_render_compat(uint32_t width, uint32_t height, const float pose[16], const float K[9],
-                       uint8_t* out) {
+/* src/renderer.cu:57-82.  Row-major uchar4, pid = y*W + x.  `contract`
+ * selects orc_get_ray_fma's evaluation of getRay (0 = source order). */
+void orc_render_compat_fma(uint32_t width, uint32_t height, const float pose[16], const float K[9],
+                           int contract, uint8_t* out) {
     const float origin[3] = {pose[12], pose[13], pose[14]};
     for (uint32_t y = 0; y < height; ++y) {
         for (uint32_t x = 0; x < width; ++x) {
             uint8_t* px = out + 4u * ((size_t)y * width + x);
             float dir[3];
-            orc_get_ray(pose, K, (float)x, (float)y, dir);
+            orc_get_ray_fma(pose, K, (float)x, (float)y, contract, dir);
             if (orc_hit_root_box(origin, dir)) {
                 px[0] = px[1] = px[2] = px[3] = 255;
                 continue;
@@ -111,6 +143,11 @@ void orc_render_compat(uint32_t width, uint32_t height, const float pose[16], co
             px[3] = 255;
         }
     }
+}
+
+void orc_render_compat(uint32_t width, uint32_t height, const float pose[16], const float K[9],
+                       uint8_t* out) {
+    orc_render_compat_fma(width, height, pose, K, 0, out);
 }
 
 /* ========================================================================== */

@@ -28,6 +28,11 @@ void orc_get_ray(const float pose[16], const float K[9], float u, float v, float
 int orc_hit_root_box(const float origin[3], const float dir[3]);
 void orc_render_compat(uint32_t width, uint32_t height, const float pose[16], const float K[9],
                        uint8_t* out_rgba8);
+/* nvcc-style FMA contraction of getRay (contract 1 or 2; 0 = as above) */
+void orc_get_ray_fma(const float pose[16], const float K[9], float u, float v, int contract,
+                     float dir_out[3]);
+void orc_render_compat_fma(uint32_t width, uint32_t height, const float pose[16], const float K[9],
+                           int contract, uint8_t* out_rgba8);
 
 /* ---- synthetic scene ----------------------------------------------------- */
 void orc_generate_spheres(uint32_t n, uint32_t seed, float* spheres, uint32_t* albedo);

@@ -31,6 +31,7 @@ RT_FLAG_RADIANCE = 1 << 2
 RT_FLAG_NO_SHADOWS = 1 << 3
 RT_FLAG_HOST_BUILD = 1 << 4
 RT_FLAG_PROGRESSIVE = 1 << 5
+RT_FLAG_COMPAT_FMA = 1 << 6
 RT_BUILDER_DEVICE = 0
 RT_BUILDER_HOST = 1
 RT_TILE_SKIP = 0xFFFFFFFF  # rt_unpack_tiles: a padding slot, not copied

@@ -3,6 +3,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import numpy as np
+
 SEED = 0x2545F491
 
 
@@ -17,6 +19,7 @@ class RenderConfig:
     gpus: int
     mode: str
     note: str
+    scene: str = "uniform"  # sphere generator: "uniform"  or "clustered"
 
     @property
     def pixels(self) -> int:
@@ -33,7 +36,36 @@ CONFIGS = {
                        "64 spp, 100k spheres, 64x64 tiles across 8 GPUs + RCCL gather"),
     "c5": RenderConfig("c5", 1920, 1080, 256, 1_000_000, 12, 1, "scene",
                        "256 spp, 1M spheres, depth-12 octree (compaction stress)"),
+    # C5 with a tree that actually reaches depth 12 (BASELINE config 5 "deep
+    # (depth-12) octree"): uniform centres stop splitting at depth 8, so the
+    # same 1M spheres are drawn around 64 clusters (clustered_spheres)
+    "c5d": RenderConfig("c5d", 1920, 1080, 256, 1_000_000, 12, 1, "scene",
+                        "256 spp, 1M clustered spheres, octree reaching depth 12", "clustered"),
 }
+
+
+def clustered_spheres(n: int, seed: int = SEED, clusters: int = 64, sigma: float = 0.03):
+    """n spheres around `clusters` Gaussian clusters (sd `sigma`) whose centres
+    are uniform in [0.15, 1.13]^3, clipped to the root box; radii and albedo
+    as SURVEY 8d D2 (0.02 (1000/n)^(1/3) U[0.5, 1]).  numpy PCG64 from `seed`:
+    the same arrays on every machine.  At 1M spheres the octree (leaf capacity
+    8, max depth 12) reaches depth 12: 1.77 M nodes, 5.9 M leaf references."""
+    g = np.random.default_rng(seed)
+    centres = g.uniform(0.15, 1.13, (clusters, 3))
+    which = g.integers(0, clusters, n)
+    c = np.clip(centres[which] + g.normal(0.0, sigma, (n, 3)), 0.0, 1.28)
+    r = 0.02 * (1000.0 / max(n, 1)) ** (1.0 / 3.0) * g.uniform(0.5, 1.0, n)
+    sp = np.ascontiguousarray(np.concatenate([c, r[:, None]], 1), dtype=np.float32)
+    al = (g.integers(0, 1 << 24, n, dtype=np.uint32) | np.uint32(0xFF000000)).astype(np.uint32)
+    return sp, al
+
+
+def scene_spheres(cfg: "RenderConfig", seed: int = SEED):
+    """The sphere list of a config (its generator, its count)."""
+    if cfg.scene == "clustered":
+        return clustered_spheres(cfg.n_spheres, seed)
+    from .renderer import generate_spheres
+    return generate_spheres(cfg.n_spheres, seed)
 
 LIGHT_DIR = (1.0, 1.0, -1.0)  # direction the light travels (SURVEY.md 8d: normalize(1,1,-1))
 AMBIENT = 0.1

@@ -155,6 +155,7 @@ void fill_frame_args(rt_renderer* r, FrameArgs& a) {
     if (r->cfg.flags & RT_FLAG_NO_JITTER) jitter = false;
     a.jitter = jitter ? 1u : 0u;
     a.shadows = (r->cfg.flags & RT_FLAG_NO_SHADOWS) ? 0u : 1u;
+    a.contract = (r->cfg.flags & RT_FLAG_COMPAT_FMA) ? 1u : 0u;
     const float* ld = r->cfg.light_dir;
     const float ll = sqrtf(ld[0] * ld[0] + ld[1] * ld[1] + ld[2] * ld[2]);
     a.L[0] = -(ld[0] / ll);

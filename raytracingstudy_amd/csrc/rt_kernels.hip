@@ -74,9 +74,30 @@ __device__ __forceinline__ bool hit_root_box(const float o[3], float d0, float d
     return fmaxf(fmaxf(tx0, ty0), tz0) < fminf(fminf(tx1, ty1), tz1);
 }
 
-__device__ __forceinline__ uint32_t compat_pixel(const CamArgs& cam, uint32_t x, uint32_t y) {
+// getRay as the reference BINARY evaluates it: nvcc's default -fmad=true
+// contracts include/camera.h:31-34 (dz = 1 folds; the DAG combiner fuses an
+// fadd of two products through its first operand).  Same operations as
+// oracle.c:orc_get_ray_fma(contract = 1).
+__device__ __forceinline__ void get_ray_fma(const CamArgs& c, float u, float v, float& wx,
+                                            float& wy, float& wz) {
+    const float dx = (u - c.K[2]) / c.K[0];
+    const float dy = (v - c.K[5]) / c.K[4];
+    wx = fmaf(c.R[0], dx, c.R[3] * dy) + c.R[6];
+    wy = fmaf(c.R[1], dx, c.R[4] * dy) + c.R[7];
+    wz = fmaf(c.R[2], dx, c.R[5] * dy) + c.R[8];
+    const float len = sqrtf(fmaf(wz, wz, fmaf(wx, wx, wy * wy)));
+    wx /= len;
+    wy /= len;
+    wz /= len;
+}
+
+__device__ __forceinline__ uint32_t compat_pixel(const CamArgs& cam, uint32_t x, uint32_t y,
+                                                 uint32_t contract) {
     float d0, d1, d2;
-    get_ray(cam, static_cast<float>(x), static_cast<float>(y), d0, d1, d2);
+    if (contract)
+        get_ray_fma(cam, static_cast<float>(x), static_cast<float>(y), d0, d1, d2);
+    else
+        get_ray(cam, static_cast<float>(x), static_cast<float>(y), d0, d1, d2);
     if (hit_root_box(cam.o, d0, d1, d2)) return 0xFFFFFFFFu;
     const uint32_t g = static_cast<uint32_t>(sat(d1) * 255.0f);
     const uint32_t b = static_cast<uint32_t>(sat(d2) * 255.0f);
@@ -88,7 +109,7 @@ __global__ void __launch_bounds__(kBlockThreads) compat_kernel(FrameArgs a) {
     const uint32_t x = blockIdx.x * 64u + (threadIdx.x & 63u);
     const uint32_t y = blockIdx.y * 4u + (threadIdx.x >> 6);
     if (x >= a.W || y >= a.H) return;
-    __builtin_nontemporal_store(compat_pixel(a.cam, x, y), a.out8 + (size_t)y * a.W + x);
+    __builtin_nontemporal_store(compat_pixel(a.cam, x, y, a.contract), a.out8 + (size_t)y * a.W + x);
 }
 
 // Tile-packed compat: block = 64 x 4 strip of one tile.
@@ -102,7 +123,7 @@ __global__ void __launch_bounds__(kBlockThreads) compat_tiles_kernel(FrameArgs a
     const uint32_t tile = a.tiles[k];
     const uint32_t x = (tile % a.tiles_x) * ts + lx;
     const uint32_t y = (tile / a.tiles_x) * ts + ly;
-    const uint32_t v = (x < a.W && y < a.H) ? compat_pixel(a.cam, x, y) : 0u;
+    const uint32_t v = (x < a.W && y < a.H) ? compat_pixel(a.cam, x, y, a.contract) : 0u;
     a.out8[(size_t)k * ts * ts + ly * ts + lx] = v;
 }
 

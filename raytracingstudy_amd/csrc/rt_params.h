@@ -135,6 +135,7 @@ struct FrameArgs {
     uint32_t seedmix;   // mix32(seed ^ 0x9E3779B9)
     uint32_t jitter;
     uint32_t shadows;
+    uint32_t contract;  // compat: 1 = getRay with nvcc-style FMA contraction (RT_FLAG_COMPAT_FMA)
     float L[3];         // unit vector toward the light
     float ambient;
     float inv_spp;      // 1 / samples in the image (all accumulated frames)

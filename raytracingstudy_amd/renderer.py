@@ -106,7 +106,8 @@ class KernelRenderer:
                  shadows: bool = True, radiance: bool = False,
                  light_dir: Sequence[float] = (1.0, 1.0, -1.0), ambient: float = 0.1,
                  variant: int = 0, opt_off: int = 0, host_build: bool = False,
-                 progressive: bool = False, cell_table: Optional[int] = None):
+                 progressive: bool = False, cell_table: Optional[int] = None,
+                 compat_fma: bool = False):
         lib = _lib.load()
         cfg = RtConfig()
         lib.rt_config_default(ctypes.byref(cfg))
@@ -128,6 +129,8 @@ class KernelRenderer:
             flags |= RT_FLAG_HOST_BUILD
         if progressive:
             flags |= RT_FLAG_PROGRESSIVE
+        if compat_fma:
+            flags |= _lib.RT_FLAG_COMPAT_FMA
         flags |= (int(variant) & 0xF) << _lib.RT_FLAG_VARIANT_SHIFT
         flags |= (int(opt_off) & 0xFF) << _lib.RT_FLAG_OPT_SHIFT
         # cell_table: None = depth chosen from the tree, 0 = no table, k = depth k

@@ -55,6 +55,34 @@ def test_compat_byte_exact(gpu, oracle, w, h, posename):
     assert np.array_equal(img, ref)
 
 
+@pytest.mark.parametrize("w,h", [(256, 256), (1920, 1080)])
+@pytest.mark.parametrize("posename", ["default", "yawed", "fuzz1", "fuzz2", "fuzz7"])
+def test_compat_fma_contraction_byte_exact(gpu, oracle, w, h, posename):
+    """RT_FLAG_COMPAT_FMA: getRay evaluated with the FMA contraction nvcc's
+    default -fmad=true gives the reference binary (include/camera.h:31-34),
+    byte-exact against the oracle's orc_render_compat_fma(contract=1); and it
+    differs from the uncontracted image by +-1 in a G or B byte on a few
+    pixels at most (tools/compat_fma_gap.py: 102 bytes over 36 poses at 1080p)."""
+    if posename.startswith("fuzz"):
+        seed = int(posename[4:])
+        g = np.random.default_rng(1000 + seed)
+        g.integers(1, 300), g.integers(1, 200)
+        pose = display_pose(tuple(g.uniform(-2.0, 3.3, 3)), float(g.uniform(-180, 180)),
+                            float(g.uniform(-89, 89)))
+    else:
+        pose = {"default": default_pose(), "yawed": display_pose((0.3, 0.9, 2.5), 23.0, -11.0)}[posename]
+    with rt.KernelRenderer(w, h, mode="compat", compat_fma=True) as r:
+        r.resize(w, h)
+        r.setPosition(pose)
+        r.render()
+        img = r.readback()
+        _, K = r.camera()
+    assert np.array_equal(img, oracle.render_compat_fma(w, h, pose, K, 1))
+    plain = oracle.render_compat(w, h, pose, K)
+    assert np.abs(img.astype(int) - plain).max() <= 1
+    assert (img != plain).sum() <= 16
+
+
 def test_compat_reference_intrinsic_k0(gpu, oracle):
     # before any resize the reference uses K0 (src/renderer.cu:87)
     pose = default_pose()
@@ -264,6 +292,24 @@ def test_scene_c5_rows(gpu, oracle):
     assert (info["n_nodes"], info["n_prim_refs"]) == (oinfo["n_nodes"], oinfo["n_prim_refs"])
     assert info["cell_table_depth"] == 6
     rows = np.arange(5, 1080, 16)
+    assert np.array_equal(img[rows], ref8[rows])
+    assert np.array_equal(rad[rows], ref32[rows])
+
+
+def test_scene_c5_deep_rows(gpu, oracle):
+    """C5d: 1M clustered spheres whose octree reaches depth 12 (BASELINE config
+    5's "deep (depth-12) octree"; walk depths 9-12 and the cell table at scale),
+    1920x1080, 256 spp, every 16th row from row 3 (68 rows, 1/16 of the
+    frame) bit-exact; the resolution-driven depth limit is src/renderer.cu:134-136's."""
+    c = rt.CONFIGS["c5d"]
+    sp, al = rt.configs.scene_spheres(c)
+    img, rad, st, info, ref8, ref32, cnt, oinfo = _scene_pair(
+        oracle, c.n_spheres, c.width, c.height, c.spp, depth=c.max_depth, row_step=16,
+        row_phase=3, spheres=(sp, al))
+    assert info["depth_reached"] == oinfo["depth_reached"] == 12
+    assert (info["n_nodes"], info["n_prim_refs"]) == (oinfo["n_nodes"], oinfo["n_prim_refs"])
+    rows = np.arange(3, c.height, 16)
+    assert len(rows) == 68
     assert np.array_equal(img[rows], ref8[rows])
     assert np.array_equal(rad[rows], ref32[rows])
 
