@@ -156,14 +156,22 @@ KERNEL_SOURCES = ("csrc/rt_kernels.hip", "csrc/rt_params.h", "csrc/Makefile")
 
 
 def kernel_source_id() -> str:
-    """sha256 (first 16 hex digits) of KERNEL_SOURCES: stamps profiles/ PMC
-    summaries (tools/pmc_traffic.py) so bench.py uses counters only for the
-    kernel they were collected on."""
+    """sha256 (first 16 hex digits) of KERNEL_SOURCES with comments and
+    whitespace removed: stamps profiles/ PMC summaries (tools/pmc_traffic.py)
+    so bench.py uses counters only for the kernel code they were collected on."""
     import hashlib
+    import re
     h = hashlib.sha256()
     for rel in KERNEL_SOURCES:
-        with open(os.path.join(_HERE, rel), "rb") as f:
-            h.update(rel.encode() + b"\0" + f.read())
+        with open(os.path.join(_HERE, rel), encoding="utf-8") as f:
+            src = f.read()
+        # code only: comments and layout do not change the machine code
+        src = re.sub(r"/\*.*?\*/", " ", src, flags=re.S)
+        src = re.sub(r"//[^\n]*", " ", src)
+        if rel.endswith("Makefile"):
+            src = re.sub(r"#[^\n]*", " ", src)
+        src = " ".join(src.split())
+        h.update(rel.encode() + b"\0" + src.encode())
     return h.hexdigest()[:16]
 
 

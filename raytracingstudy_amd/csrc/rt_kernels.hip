@@ -77,7 +77,7 @@ __device__ __forceinline__ bool hit_root_box(const float o[3], float d0, float d
 // getRay as the reference BINARY evaluates it: nvcc's default -fmad=true
 // contracts include/camera.h:31-34 (dz = 1 folds; the DAG combiner fuses an
 // fadd of two products through its first operand).  Same operations as
-// oracle.c:orc_get_ray_fma(contract = 1).
+// the oracle's contracted getRay, contract = 1.
 __device__ __forceinline__ void get_ray_fma(const CamArgs& c, float u, float v, float& wx,
                                             float& wy, float& wz) {
     const float dx = (u - c.K[2]) / c.K[0];
