@@ -226,6 +226,22 @@ int rt_render(rt_renderer* r, void* dev_rgba8, void* stream, rt_stats* stats);
  * (src/renderer.cu:145-151).  NULL unbinds (render into the internal
  * framebuffer).  The resource stays owned by the caller. */
 int rt_bind_graphics_resource(rt_renderer* r, void* hip_graphics_resource);
+/* The same per-frame map -> render -> unmap cycle for a display buffer the
+ * caller's toolkit owns (a GL PBO, Vulkan/EGL external memory, a swap-chain
+ * image): rt_render(r, NULL, stream, stats) calls ops->map(user, stream, &ptr,
+ * &bytes) on the frame's stream, fails with RT_E_INVALID (after unmapping) if
+ * bytes < W*H*4, renders into ptr and calls ops->unmap(user, stream) after
+ * the launch, also when the render itself failed.  map/unmap return 0 on
+ * success; a failing map must leave the buffer unmapped, and rt_render then
+ * returns RT_E_HIP.  rt_bind_graphics_resource(r, res) is this call with the
+ * built-in HIP graphics-interop ops (hipGraphicsMapResources, ...GetMappedPointer,
+ * hipGraphicsUnmapResources) and user = res.  ops == NULL unbinds; *ops is
+ * copied.  SURVEY.md 8f F2; replaces src/renderer.cu:145-151. */
+typedef struct rt_display_ops {
+    int (*map)(void* user, void* stream, void** dev_ptr, size_t* bytes);
+    int (*unmap)(void* user, void* stream);
+} rt_display_ops;
+int rt_bind_display(rt_renderer* r, const rt_display_ops* ops, void* user);
 /* Render only the listed image tiles (tile_size x tile_size, row-major tile
  * ids over ceil(W/ts) x ceil(H/ts)) into a packed device buffer of
  * n_tiles*ts*ts*4 bytes: tile k's pixel (lx,ly) at byte 4*(k*ts*ts + ly*ts + lx);

@@ -70,6 +70,9 @@ public:
     void setGraphicsResource(void* graphics_resource) {
         check(rt_bind_graphics_resource(r_, graphics_resource), r_);
     }
+    // any toolkit's display buffer: render() maps, fills and unmaps it per
+    // frame through `ops` (rt_bind_display; nullptr unbinds)
+    void setDisplay(const rt_display_ops* ops, void* user) { check(rt_bind_display(r_, ops, user), r_); }
     // resize(int, int) (src/renderer.cu:155-187)
     void resize(int width, int height) {
         check(rt_resize(r_, static_cast<uint32_t>(width), static_cast<uint32_t>(height)), r_);

@@ -111,6 +111,17 @@ class RtSceneInfo(ctypes.Structure):
         return d
 
 
+# rt_display_ops: int map(void* user, void* stream, void** ptr, size_t* bytes),
+# int unmap(void* user, void* stream)
+DISPLAY_MAP = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t))
+DISPLAY_UNMAP = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)
+
+
+class RtDisplayOps(ctypes.Structure):
+    _fields_ = [("map", DISPLAY_MAP), ("unmap", DISPLAY_UNMAP)]
+
+
 # every symbol declared in include/rt.h, with (restype, argtypes)
 _P = ctypes.c_void_p
 _u32 = ctypes.c_uint32
@@ -138,6 +149,7 @@ SIGNATURES = {
     "rt_generate_spheres": (_int, [_u32, _u32, _P, _P]),
     "rt_render": (_int, [_P, _P, _P, ctypes.POINTER(RtStats)]),
     "rt_bind_graphics_resource": (_int, [_P, _P]),
+    "rt_bind_display": (_int, [_P, ctypes.POINTER(RtDisplayOps), _P]),
     "rt_render_tiles": (_int, [_P, _P, _u32, _u32, _P, _P, ctypes.POINTER(RtStats)]),
     "rt_unpack_tiles": (_int, [_P, _P, _P, _u32, _u32, _P, _P]),
     "rt_reset_accumulation": (_int, [_P]),

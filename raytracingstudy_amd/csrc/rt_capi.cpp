@@ -78,8 +78,11 @@ struct rt_renderer {
     };
     std::vector<TileList> tile_lists;
     uint64_t tile_clock = 0;
-    // GL interop: the Displayer's registered PBO (hipGraphicsGLRegisterBuffer)
-    hipGraphicsResource_t gfx = nullptr;
+    // display buffer mapped per frame: the Displayer's
+    // registered GL PBO through the HIP graphics ops, or a caller's ops
+    rt_display_ops disp{};
+    void* disp_user = nullptr;
+    bool gl_disp = false;  // disp are the built-in HIP graphics-interop ops
     // scene: the sphere list lives in d_spheres/d_albedo; `spheres` is a host
     // copy when the scene came from host memory (host builder input)
     uint32_t n_spheres = 0;
@@ -797,34 +800,69 @@ int rt_render(rt_renderer* r, void* dev_rgba8, void* stream, rt_stats* stats) {
     fill_frame_args(r, a);
     a.out8 = dev_rgba8 ? static_cast<uint32_t*>(dev_rgba8) : r->fb.p;
     a.out32 = (r->cfg.flags & RT_FLAG_RADIANCE) ? r->rad.p : nullptr;
-    if (dev_rgba8 || !r->gfx) return do_render(r, a, stream, stats);
+    if (dev_rgba8 || !r->disp.map) return do_render(r, a, stream, stats);
     // the reference's render(): map the PBO, launch into it, unmap
     // (src/renderer.cu:145-151)
     hipStream_t hs = stream ? static_cast<hipStream_t>(stream) : r->stream;
-    RT_HIP(r, hipGraphicsMapResources(1, &r->gfx, hs));
+    if ((st = order_after_last(r, hs))) return st;
     void* ptr = nullptr;
     size_t bytes = 0;
-    hipError_t e = hipGraphicsResourceGetMappedPointer(&ptr, &bytes, r->gfx);
-    if (e == hipSuccess && bytes < (size_t)r->W * r->H * 4) {
-        (void)hipGraphicsUnmapResources(1, &r->gfx, hs);
-        return fail(r, RT_E_INVALID, "rt_render: bound graphics resource smaller than W*H*4 bytes");
+    const int em = r->disp.map(r->disp_user, hs, &ptr, &bytes);
+    if (em != 0) {
+        std::string m = "rt_render: display buffer map failed (" + std::to_string(em) + ")";
+        if (r->gl_disp) m += std::string(": ") + hipGetErrorString(static_cast<hipError_t>(em));
+        return fail(r, RT_E_HIP, m);
     }
-    if (e != hipSuccess) {
-        (void)hipGraphicsUnmapResources(1, &r->gfx, hs);
-        return hip_fail(r, e, "hipGraphicsResourceGetMappedPointer");
+    if (!ptr || bytes < (size_t)r->W * r->H * 4) {
+        (void)r->disp.unmap(r->disp_user, hs);
+        return fail(r, RT_E_INVALID, "rt_render: display buffer smaller than W*H*4 bytes");
     }
     a.out8 = static_cast<uint32_t*>(ptr);
     st = do_render(r, a, hs, stats);
-    hipError_t eu = hipGraphicsUnmapResources(1, &r->gfx, hs);
+    const int eu = r->disp.unmap(r->disp_user, hs);
     if (st) return st;
-    if (eu != hipSuccess) return hip_fail(r, eu, "hipGraphicsUnmapResources");
+    if (eu != 0) {
+        std::string m = "rt_render: display buffer unmap failed (" + std::to_string(eu) + ")";
+        if (r->gl_disp) m += std::string(": ") + hipGetErrorString(static_cast<hipError_t>(eu));
+        return fail(r, RT_E_HIP, m);
+    }
+    return RT_OK;
+}
+
+namespace {
+// built-in ops over a hipGraphicsResource_t (hipGraphicsGLRegisterBuffer);
+// the status is the hipError_t
+int gl_map(void* user, void* stream, void** ptr, size_t* bytes) {
+    hipGraphicsResource_t res = static_cast<hipGraphicsResource_t>(user);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e = hipGraphicsMapResources(1, &res, s);
+    if (e != hipSuccess) return static_cast<int>(e);
+    e = hipGraphicsResourceGetMappedPointer(ptr, bytes, res);
+    if (e != hipSuccess) (void)hipGraphicsUnmapResources(1, &res, s);
+    return static_cast<int>(e);
+}
+int gl_unmap(void* user, void* stream) {
+    hipGraphicsResource_t res = static_cast<hipGraphicsResource_t>(user);
+    return static_cast<int>(hipGraphicsUnmapResources(1, &res, static_cast<hipStream_t>(stream)));
+}
+}  // namespace
+
+int rt_bind_display(rt_renderer* r, const rt_display_ops* ops, void* user) {
+    if (!r) return fail(r, RT_E_INVALID, "rt_bind_display: null handle");
+    if (ops && (!ops->map || !ops->unmap))
+        return fail(r, RT_E_INVALID, "rt_bind_display: map and unmap are both required");
+    r->disp = ops ? *ops : rt_display_ops{};
+    r->disp_user = ops ? user : nullptr;
+    r->gl_disp = false;
     return RT_OK;
 }
 
 int rt_bind_graphics_resource(rt_renderer* r, void* resource) {
     if (!r) return fail(r, RT_E_INVALID, "rt_bind_graphics_resource: null handle");
-    r->gfx = static_cast<hipGraphicsResource_t>(resource);
-    return RT_OK;
+    static const rt_display_ops kGl = {gl_map, gl_unmap};
+    const int st = rt_bind_display(r, resource ? &kGl : nullptr, resource);
+    r->gl_disp = resource != nullptr;
+    return st;
 }
 
 int rt_render_tiles(rt_renderer* r, const uint32_t* tile_ids, uint32_t n_tiles, uint32_t ts,

@@ -186,6 +186,37 @@ class KernelRenderer:
         check(self._lib.rt_set_octree(self._h, _fptr(a), _fptr(b), float(resolution)), self._h)
 
     # -- additions ------------------------------------------------------------
+    def bind_display(self, map_fn=None, unmap_fn=None) -> None:
+        """A display buffer mapped per frame (rt_bind_display): the
+        reference's render() maps its PBO, renders into it and unmaps it
+        (src/renderer.cu:145-151).  map_fn(stream) -> (device_ptr, nbytes) or
+        None (failure); unmap_fn(stream) -> None, or False on failure.  Called
+        with no arguments it unbinds (render into the internal framebuffer)."""
+        if map_fn is None:
+            self._display = None
+            check(self._lib.rt_bind_display(self._h, None, None), self._h)
+            return
+
+        def _map(_user, stream, ptr, nbytes):
+            try:
+                got = map_fn(stream or 0)
+            except Exception:  # an exception must not unwind through C
+                return 1
+            if got is None:
+                return 1
+            ptr[0], nbytes[0] = int(got[0]), int(got[1])
+            return 0
+
+        def _unmap(_user, stream):
+            try:
+                return 1 if unmap_fn(stream or 0) is False else 0
+            except Exception:
+                return 1
+
+        ops = _lib.RtDisplayOps(_lib.DISPLAY_MAP(_map), _lib.DISPLAY_UNMAP(_unmap))
+        self._display = ops  # the C side keeps raw function pointers: keep them alive
+        check(self._lib.rt_bind_display(self._h, ctypes.byref(ops), None), self._h)
+
     def set_scene(self, spheres: np.ndarray, albedo: Optional[np.ndarray] = None, *,
                   root_min=(0.0, 0.0, 0.0), root_max=(1.28, 1.28, 1.28),
                   resolution: float = 0.01, max_depth: int = 0, leaf_capacity: int = 8) -> dict:

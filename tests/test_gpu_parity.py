@@ -463,7 +463,6 @@ def test_graphics_resource_binding_plumbing(gpu):
     """F2 plumbing (a GL context cannot be created on the GPU box): binding NULL
     keeps rendering into the internal framebuffer; an explicit device pointer
     always wins over a bound resource."""
-    import ctypes
     import torch
     sp, al = rt.generate_spheres(1000, rt.SEED)
     with rt.KernelRenderer(64, 48, mode="scene", spp=2) as r:
@@ -482,6 +481,98 @@ def test_graphics_resource_binding_plumbing(gpu):
         r.synchronize()
         assert np.array_equal(buf.cpu().numpy().reshape(48, 64, 4), ref)
     assert lib.rt_bind_graphics_resource(None, None) == rt._lib.RT_E_INVALID
+
+
+def test_display_map_render_unmap(gpu, oracle):
+    """F2's per-frame cycle (src/renderer.cu:145-151: map the PBO, render into
+    the mapped pointer, unmap) through rt_bind_display, the code path the GL
+    binding takes with HIP's graphics-interop ops: the frame lands in the
+    mapped buffer bit-exact against the oracle; map and unmap run once per
+    frame on the frame's stream, in that order; the size check, a failing map,
+    a failing unmap and a failing render are reported and never leave the
+    buffer mapped."""
+    import torch
+    w, h = 64, 48
+    sp, al = rt.generate_spheres(1000, rt.SEED)
+    buf = torch.zeros(w * h * 4, dtype=torch.uint8, device="cuda")
+    log = []
+    state = {"bytes": w * h * 4, "map_ok": True, "unmap_ok": True}
+
+    def map_fn(stream):
+        log.append(("map", stream))
+        return (buf.data_ptr(), state["bytes"]) if state["map_ok"] else None
+
+    def unmap_fn(stream):
+        log.append(("unmap", stream))
+        return state["unmap_ok"]
+
+    with rt.KernelRenderer(w, h, mode="scene", spp=2) as r:
+        r.resize(w, h)
+        r.setPosition(scene_pose())
+        r.set_scene(sp, al)
+        _, K = r.camera()
+        ref, _, _ = oracle.Scene(sp, al).render(w, h, scene_pose(), K, spp=2, radiance=False)
+        torch.cuda.synchronize()
+        r.bind_display(map_fn, unmap_fn)
+        r.render()
+        r.synchronize()
+        assert [e[0] for e in log] == ["map", "unmap"] and log[0][1] == log[1][1] != 0
+        assert np.array_equal(buf.cpu().numpy().reshape(h, w, 4), ref)
+        # on a caller's (non-blocking) stream, with stats
+        s = torch.cuda.Stream()
+        log.clear()
+        buf.zero_()
+        torch.cuda.synchronize()
+        st = r.render(stream=s.cuda_stream, stats=True)
+        assert log == [("map", s.cuda_stream), ("unmap", s.cuda_stream)]
+        assert st.primary_rays == w * h * 2
+        s.synchronize()
+        assert np.array_equal(buf.cpu().numpy().reshape(h, w, 4), ref)
+        # an explicit pointer wins: no map
+        log.clear()
+        other = torch.zeros_like(buf)
+        torch.cuda.synchronize()
+        r.render(other.data_ptr())
+        r.synchronize()
+        assert log == [] and np.array_equal(other.cpu().numpy().reshape(h, w, 4), ref)
+        # too small: refused, unmapped
+        state["bytes"] = w * h * 4 - 1
+        with pytest.raises(rt._lib.RtError) as e:
+            r.render()
+        assert e.value.code == rt._lib.RT_E_INVALID and [x[0] for x in log] == ["map", "unmap"]
+        # map fails: RT_E_HIP, nothing to unmap
+        state["bytes"], state["map_ok"] = w * h * 4, False
+        log.clear()
+        with pytest.raises(rt._lib.RtError) as e:
+            r.render()
+        assert e.value.code == rt._lib.RT_E_HIP and [x[0] for x in log] == ["map"]
+        # unmap fails: the frame was rendered, the failure is reported
+        state["map_ok"], state["unmap_ok"] = True, False
+        buf.zero_()
+        torch.cuda.synchronize()
+        with pytest.raises(rt._lib.RtError) as e:
+            r.render()
+        assert e.value.code == rt._lib.RT_E_HIP
+        r.synchronize()
+        assert np.array_equal(buf.cpu().numpy().reshape(h, w, 4), ref)
+        state["unmap_ok"] = True
+        # unbound: the internal framebuffer again
+        r.bind_display()
+        log.clear()
+        r.render()
+        assert log == [] and np.array_equal(r.readback(), ref)
+        lib = rt._lib.load()
+        half = rt._lib.RtDisplayOps()
+        half.map = rt._lib.DISPLAY_MAP(lambda *a: 0)
+        assert lib.rt_bind_display(r._h, half, None) == rt._lib.RT_E_INVALID
+    # a render that fails after the map still unmaps
+    with rt.KernelRenderer(w, h, mode="scene", spp=2) as r2:
+        r2.bind_display(map_fn, unmap_fn)
+        log.clear()
+        with pytest.raises(rt._lib.RtError) as e:
+            r2.render()  # no scene
+        assert e.value.code == rt._lib.RT_E_NOSCENE
+        assert [x[0] for x in log] == ["map", "unmap"]
 
 
 @pytest.mark.parametrize("spp", [65, 127])
