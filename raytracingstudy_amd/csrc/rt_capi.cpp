@@ -408,7 +408,7 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     // per-wave timeline to $RT_TIMELINE_FILE
     static unsigned long long* tl = nullptr;
     const size_t tl_waves = 1u << 16;
-    const size_t tl_words = tl_waves * 4 + (2u << 22) + tl_waves * 2;  // per wave, per unit, phases
+    const size_t tl_words = tl_waves * 4 + (3u << 22) + tl_waves * 2;  // per wave, per unit, phases
     const char* tl_file = getenv("RT_TIMELINE_FILE");
     if (tl_file) {
         if (!tl) RT_HIP(r, hipMalloc(reinterpret_cast<void**>(&tl), tl_words * 8));

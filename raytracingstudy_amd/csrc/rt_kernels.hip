@@ -1251,7 +1251,13 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
         const uint32_t sb_grid = nsx * nsy;  // superblocks per grid
         const uint32_t n_sb = kTiles ? a.n_tiles * sb_grid : sb_grid;
         const uint32_t grp = blockIdx.x & 7u;
-        for (uint32_t hop = 0; hop < 8u; ++hop) {
+        // Stealing (taking tickets of the next ranges once the own range is
+        // dry) only for frames of fewer than 2 superblocks per range: stolen
+        // units run on an XCD whose L2 holds another region, 3-6x slower than
+        // at home, and their atomics pile onto the last ranges' heads; without
+        // it C3 is -1.9% and its 1/8 tile share -10% (profiles/r02/steal_ab.log)
+        const uint32_t hops = (n_sb >= 16u && gridDim.x >= 8u) ? 1u : 8u;
+        for (uint32_t hop = 0; hop < hops; ++hop) {
             const uint32_t q = (grp + hop) & 7u;
             // range q = superblocks q, q + 8, q + 16, ... (4096 units each):
             // every XCD's share is spread over the whole image, so the ranges
@@ -1294,11 +1300,16 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
                 shade_wave_tile<kTiles, kVar, kChunk, kStats, kProg, kLeafMode>(
                     a, acc, stk, lbuf, ox, oy, k, olx, oly, n_primary, n_shadow, n_nodes, n_prims, bs);
 #ifdef RT_TIMELINE
-                // per unit {start, end} after the 65536 per-wave records
-                const unsigned long long uid = (unsigned long long)sb * 4096u + (cur & 4095u);
+                // per unit {start, end, hw_id << 32 | xcc << 16 | wave index}
+                // after the 65536 per-wave records
+                const unsigned long long uid = (unsigned long long)sb * 4096u + b * 64u + w;
                 if (a.timeline && (threadIdx.x & 63u) == 0 && uid < (1ull << 22)) {
-                    a.timeline[4ull * 65536 + 2 * uid] = tu0;
-                    a.timeline[4ull * 65536 + 2 * uid + 1] = wall_clock64();
+                    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+                    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // XCC_ID
+                    a.timeline[4ull * 65536 + 3 * uid] = tu0;
+                    a.timeline[4ull * 65536 + 3 * uid + 1] = wall_clock64();
+                    a.timeline[4ull * 65536 + 3 * uid + 2] =
+                        ((unsigned long long)hw << 32) | (xcc << 16) | (blockIdx.x * 4u + wave);
                 }
 #endif
             }
@@ -1439,6 +1450,20 @@ static uint32_t resident_blocks(K kernel, size_t lds) {
     return n;
 }
 
+static uint32_t cus_of_device() {
+    static std::mutex mu;
+    static std::vector<std::pair<int, uint32_t>> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> g(mu);
+    for (const auto& e : cache)
+        if (e.first == dev) return e.second;
+    hipDeviceProp_t prop;
+    const uint32_t n = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
+    cache.push_back({dev, n});
+    return n;
+}
+
 constexpr size_t kOneSppLds = (160u * 1024u / 3u) & ~size_t(15);  // 3 workgroups per CU
 
 // Block tiles in the frame (or in the packed tile list) for block-tile side b.
@@ -1475,7 +1500,8 @@ static void launch_persistent(K kernel, const FrameArgs& a_in, uint32_t, size_t 
 
 // Per-wave queue launch: grid = resident workgroups, capped by the work.
 template <typename K>
-static void launch_waveq(K kernel, const FrameArgs& a, size_t lds, hipStream_t st) {
+static void launch_waveq(K kernel, const FrameArgs& a, size_t lds, hipStream_t st,
+                         uint32_t per_simd = 7) {
     const uint32_t res = resident_blocks(kernel, lds);
     uint64_t units;
     if (a.tiles)
@@ -1484,7 +1510,14 @@ static void launch_waveq(K kernel, const FrameArgs& a, size_t lds, hipStream_t s
         units = (uint64_t)((a.W + a.tw - 1) / a.tw) * ((a.H + a.th - 1) / a.th);
     // (the grid only sizes the launch; padding units of edge blocks are skipped)
     const uint64_t want = (units + kBlockThreads / 64 - 1) / (kBlockThreads / 64);
-    const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(res, want)));
+    // The occupancy query counts 8 workgroups per CU for the 7-wave builds
+    // (60-65 VGPRs), but their 94 SGPRs leave room for 7: the 8th per CU
+    // only starts when another exits, finds nothing and adds 8 queue atomics
+    // to the tail (profiles/r02/timeline_hwid.log).  Capped at the build's
+    // waves per SIMD: C3 -0.8%, 1/8 share -5% (profiles/r02/steal_ab.log)
+    const uint64_t cap = per_simd ? static_cast<uint64_t>(cus_of_device()) * per_simd : res;
+    const uint32_t grid =
+        static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(std::min<uint64_t>(res, cap), want)));
     FrameArgs b = a;
     if (!((a.sc.opt >> kOptChunkShift) & 7u)) {
         // auto ticket size, second half: a small launch (a multi-GPU share)
@@ -1560,42 +1593,42 @@ static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStr
         case kVariantWaveQLds:  // 13 + wave-uniform leaves staged through LDS
             if (a.count_work)
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true, 1>,
-                             a, lds, st);
+                             a, lds, st, 0);
             else
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true, 1>,
-                             a, lds, st);
+                             a, lds, st, 0);
             break;
         case kVariantWaveQLane:  // 13 + one-lane loads broadcast by readfirstlane
             if (a.count_work)
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true, 3>,
-                             a, lds, st);
+                             a, lds, st, 0);
             else
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true, 3>,
-                             a, lds, st);
+                             a, lds, st, 0);
             break;
         case kVariantWaveQSmem:  // 13 + wave-uniform leaves read by scalar loads
             if (a.count_work)
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true, 2>,
-                             a, lds, st);
+                             a, lds, st, 0);
             else
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true, 2>,
-                             a, lds, st);
+                             a, lds, st, 0);
             break;
         case kVariantWaveQ6:  // 13 at the allocator's own occupancy (6 waves/SIMD)
             if (a.count_work)
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true>,
-                             a, lds, st);
+                             a, lds, st, 0);
             else
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true>,
-                             a, lds, st);
+                             a, lds, st, 0);
             break;
         case kVariantWaveQ8:  // 13 compiled for 8 waves/SIMD
             if (a.count_work)
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 8, 2, true, false, true>,
-                             a, lds, st);
+                             a, lds, st, 8);
             else
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 8, 2, false, false, true>,
-                             a, lds, st);
+                             a, lds, st, 8);
             break;
 #endif
         default:  // rejected by variant_available() before any launch

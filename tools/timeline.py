@@ -78,6 +78,7 @@ def main():
     ap.add_argument("--n", type=int, default=8)
     ap.add_argument("--frames", type=int, default=2)
     ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--dump", default="", help="save per-unit {start, end} ticks (.npz)")
     args = ap.parse_args()
     fd, path = tempfile.mkstemp(suffix=".tl")
     os.close(fd)
@@ -94,6 +95,7 @@ def main():
     slab = torch.zeros(len(share) * ts * ts * 4, dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
     out = {}
+    dumps = {"share_tiles": np.asarray(share, np.uint32)}
     for name, fn in (("full", lambda: r.render()),
                      (f"share_1_of_{args.n}", lambda: r.render_tiles(share, ts, slab.data_ptr()))):
         fn()  # warm-up
@@ -102,16 +104,22 @@ def main():
             fn()
         r.synchronize()
         raw = np.fromfile(path, dtype=np.uint64).reshape(args.frames, -1).astype(np.int64)
-        unit_end = WAVE_WORDS + (2 << 22)
+        unit_end = WAVE_WORDS + (3 << 22)
         out[name] = []
+        if args.dump:
+            dumps[name] = raw[:, WAVE_WORDS:unit_end].reshape(args.frames, -1, 3)
+            dumps[name + "_waves"] = raw[:, :WAVE_WORDS].reshape(args.frames, -1, 4)
         for i in range(args.frames):
-            sm = summarise(raw[i, :WAVE_WORDS].reshape(-1, 4), raw[i, WAVE_WORDS:unit_end].reshape(-1, 2))
+            sm = summarise(raw[i, :WAVE_WORDS].reshape(-1, 4), raw[i, WAVE_WORDS:unit_end].reshape(-1, 3)[:, :2])
             ph = raw[i, unit_end:].reshape(-1, 2).sum(0).astype(float)
             sm["phase_ticks_share"] = {"primary": round(ph[0] / max(ph.sum(), 1), 3),
                                        "shadow": round(ph[1] / max(ph.sum(), 1), 3)}
             out[name].append(sm)
         print(name, json.dumps(out[name][-1]), flush=True)
     os.unlink(path)
+    if args.dump:
+        np.savez_compressed(args.dump, **{k.replace("share_1_of_%d" % args.n, "share"): v
+                                          for k, v in dumps.items()})
     r.close()
 
 
