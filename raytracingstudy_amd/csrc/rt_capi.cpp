@@ -400,7 +400,23 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
         return fail(r, RT_E_NOSCENE, "RT_MODE_SCENE render without rt_set_scene");
     int ost;
     if ((ost = order_after_last(r, st))) return ost;
-    RT_HIP(r, hipMemsetAsync(r->counters.p, 0, kCounterWords * sizeof(unsigned long long), st));
+    // the counters and, for the wave queue, its per-XCD slot table (8 x
+    // (superblocks + 2) words after them): one buffer, one memset per frame
+    size_t words = kCounterWords;
+    a.wq_slots = nullptr;
+    a.wq_slot_stride = 0;
+    if (r->cfg.mode == RT_MODE_SCENE) {
+        const uint32_t nt = a.tiles ? a.n_tiles : 0u;
+        const uint32_t nsb = scene_superblocks(a.W, a.H, a.spp, nt, a.tile_size);
+        const uint32_t nbk = scene_blocks(a.W, a.H, a.spp, nt, a.tile_size);
+        a.wq_slot_shift = wave_queue_slot_shift(nsb, nbk);
+        a.wq_slot_stride = (a.wq_slot_shift == 12u ? nsb : nbk) + 2u;
+        words += (8u * static_cast<size_t>(a.wq_slot_stride) + 1u) / 2u;
+    }
+    if ((ost = ensure(r, r->counters, words))) return ost;
+    if (a.wq_slot_stride) a.wq_slots = reinterpret_cast<uint32_t*>(r->counters.p + kCounterWords);
+    a.counters = r->counters.p;
+    RT_HIP(r, hipMemsetAsync(r->counters.p, 0, words * sizeof(unsigned long long), st));
     a.count_work = stats ? 1u : 0u;
     if (stats) RT_HIP(r, hipEventRecord(r->ev0, st));
 #ifdef RT_TIMELINE
@@ -473,6 +489,11 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
         stats->ms = ms;
         stats->samples_per_pixel = r->cfg.mode != RT_MODE_SCENE ? 1u
                                    : a.accum ? a.spp * r->frames_accum : a.spp;
+        unsigned long long qerr = 0;
+        RT_HIP(r, hipMemcpy(&qerr, r->counters.p + kWaveQueueClaim + 1, sizeof(qerr),
+                            hipMemcpyDeviceToHost));
+        if (qerr)
+            return fail(r, RT_E_HIP, "scene kernel: wave-queue slot never published (frame incomplete)");
     }
     return RT_OK;
 }

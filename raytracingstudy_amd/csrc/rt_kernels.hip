@@ -1200,14 +1200,14 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
 // kWaveQ = false: workgroups pull bts x bts block tiles from ONE device-wide
 //   queue head (a returning atomic per tile); the tile's wave tiles are dealt
 //   to the 4 waves round-robin, and the workgroup syncs per tile.
-// kWaveQ = true: every WAVE pulls single wave tiles on its own.  The wave
-//   tiles are numbered in 8x8 blocks (spatially coherent) and split into 8
-//   contiguous ranges, one per XCD group (blockIdx % 8: blocks dealt
-//   round-robin over the 8 XCDs share one, MI355X_MICROARCH.md "Workgroup
-//   dispatch"), each with its own head on its own cache line (one head
-//   saturates near 88 dequeues/us; per-XCD heads cost ~1.1 us under load).
-//   An XCD's waves work through its region (L2 locality), then steal from the
-//   next ranges.  No workgroup barrier; the tail is one wave tile.
+// kWaveQ = true: every WAVE pulls tickets of 1-4 wave tiles on its own.  The
+//   wave tiles are numbered in 8x8 blocks (spatially coherent) of 8x8-block
+//   superblocks; whole superblocks go to XCD groups (blockIdx % 8: blocks are
+//   dealt round-robin over the 8 XCDs, MI355X_MICROARCH.md "Workgroup
+//   dispatch") in claim order, and each XCD has its own ticket head on its
+//   own cache line (one head saturates near 88 dequeues/us) over the
+//   superblocks it claimed: the two-level queue below.  No workgroup barrier;
+//   the tail is one ticket.
 //
 // kMinW = minimum waves per SIMD requested from the register allocator.
 // kProg: progressive frame (a.accum set); compiled separately so plain frames
@@ -1250,43 +1250,85 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
         const uint32_t nsx = (nbx + 7u) / 8u, nsy = (nby + 7u) / 8u;
         const uint32_t sb_grid = nsx * nsy;  // superblocks per grid
         const uint32_t n_sb = kTiles ? a.n_tiles * sb_grid : sb_grid;
-        const uint32_t grp = blockIdx.x & 7u;
-        // Stealing (taking tickets of the next ranges once the own range is
-        // dry) only for frames of fewer than 2 superblocks per range: stolen
-        // units run on an XCD whose L2 holds another region, 3-6x slower than
-        // at home, and their atomics pile onto the last ranges' heads; without
-        // it C3 is -1.9% and its 1/8 tile share -10% (profiles/r02/steal_ab.log)
-        const uint32_t hops = (n_sb >= 16u && gridDim.x >= 8u) ? 1u : 8u;
-        for (uint32_t hop = 0; hop < hops; ++hop) {
-            const uint32_t q = (grp + hop) & 7u;
-            // range q = superblocks q, q + 8, q + 16, ... (4096 units each):
-            // every XCD's share is spread over the whole image, so the ranges
-            // cost about the same and stealing is left to the very end
-            const uint32_t hi = (n_sb > q ? (n_sb - q + 7u) / 8u : 0u) * 4096u;
-            unsigned long long* head = a.counters + kWaveQueueBase + q * kWaveQueueStride;
-            const uint32_t chunk = a.wq_chunk;  // wave tiles per ticket
-            uint32_t u = hi, u_end = hi;
-            for (;;) {
-                if (u >= u_end) {  // take the next ticket
-                    uint32_t t = 0;
-                    if ((threadIdx.x & 63u) == 0) t = static_cast<uint32_t>(atomicAdd(head, 1ull));
-                    u = __builtin_amdgcn_readfirstlane(t) * chunk;
+        // Two-level queue.  Level 1 hands whole superblocks (4096 wave tiles,
+        // one 64x64 tile at 64 spp) to XCDs in claim order from one counter;
+        // level 2 is a per-XCD ticket head over the XCD's own sequence of
+        // superblocks ("slots": slot s = units [4096 s, 4096 s + 4096) of that
+        // head).  An XCD's waves thus share one image region at a time (its
+        // L2 holds that region's part of the scene), no unit ever runs on
+        // another XCD (a stolen unit runs 3-6x slower, L2-cold), and the XCDs
+        // still balance dynamically at superblock granularity (uneven scenes).
+        // The ticket holding the middle unit of slot s claims slot s + 1 half
+        // a slot early, so waves arriving at a new slot find it published;
+        // ticket 0 claims slot 0.  A claim past the last superblock publishes
+        // kSlotNone and the waves that reach it exit.  Frames of fewer than
+        // 16 superblocks claim single 8x8 blocks instead (slot = 64 units),
+        // numbered over the blocks that hold wave tiles, so a small frame
+        // spreads over all XCDs and never dequeues a superblock of padding.
+        const uint32_t q = blockIdx.x & 7u;  // this workgroup's XCD (round-robin dispatch)
+        unsigned long long* head = a.counters + kWaveQueueBase + q * kWaveQueueStride;
+        unsigned long long* claims = a.counters + kWaveQueueClaim;
+        uint32_t* slots = a.wq_slots + q * a.wq_slot_stride;
+        const uint32_t chunk = a.wq_chunk;  // wave tiles per ticket (divides 32)
+        const uint32_t ks = a.wq_slot_shift;  // 12: superblock slots, 6: block slots
+        const uint32_t nbb = nbx * nby;       // blocks per grid
+        const uint32_t n1 = ks == 12u ? n_sb : (kTiles ? a.n_tiles : 1u) * nbb;  // level-1 units
+        const uint32_t half = 1u << (ks - 1u);
+        // the current slot's grid (packed tile) and origin in wave tiles
+        uint32_t cached_s = ~0u, k = 0, sx0 = 0, sy0 = 0;
+        for (;;) {
+            uint32_t t = 0;
+            if ((threadIdx.x & 63u) == 0) t = static_cast<uint32_t>(atomicAdd(head, 1ull));
+            const uint32_t u0 = __builtin_amdgcn_readfirstlane(t) * chunk;
+            const uint32_t s = u0 >> ks, w0 = u0 & ((1u << ks) - 1u);
+            if ((threadIdx.x & 63u) == 0 && (u0 == 0u || (w0 <= half && half < w0 + chunk))) {
+                const uint32_t slot = u0 == 0u ? 0u : s + 1u;
+                const uint32_t g = static_cast<uint32_t>(atomicAdd(claims, 1ull));
+                if (slot < a.wq_slot_stride)
+                    __hip_atomic_store(slots + slot, g < n1 ? g + 1u : kSlotNone, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (s != cached_s) {  // resolve the slot's superblock or block (published, or soon)
+                uint32_t e = kSlotNone;
+                if ((threadIdx.x & 63u) == 0 && s < a.wq_slot_stride) {
+                    // the claimer holds a ticket already and publishes before it
+                    // waits on anything; the cap (~1 s) only turns a broken
+                    // invariant into a flagged, visibly wrong frame, not a hang
+                    for (uint32_t spin = 0;; ++spin) {
+                        e = __hip_atomic_load(slots + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (e != 0u) break;
+                        if (spin == (1u << 22)) {
+                            atomicOr(a.counters + kWaveQueueClaim + 1, 1ull);
+                            e = kSlotNone;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(8);
+                    }
+                }
+                e = __builtin_amdgcn_readfirstlane(e);
 #ifdef RT_TIMELINE
-                    if (u >= hi && !tl_empty) tl_empty = wall_clock64();
+                if (e == kSlotNone && !tl_empty) tl_empty = wall_clock64();
 #endif
-                    if (u >= hi) break;
-                    u_end = min(u + chunk, hi);
+                if (e == kSlotNone) break;
+                cached_s = s;
+                const uint32_t g = e - 1u;
+                if (ks == 12u) {
+                    k = kTiles ? g / sb_grid : 0u;
+                    const uint32_t sg = g - k * sb_grid;
+                    sx0 = (sg % nsx) * 64u;
+                    sy0 = (sg / nsx) * 64u;
+                } else {
+                    k = kTiles ? g / nbb : 0u;
+                    const uint32_t r = g - k * nbb;
+                    sx0 = (r % nbx) * 8u;
+                    sy0 = (r / nbx) * 8u;
                 }
-                const uint32_t cur = u++;
-                const uint32_t sb = q + 8u * (cur >> 12), b = (cur >> 6) & 63u, w = cur & 63u;
-                uint32_t k = 0, sg = sb;
-                if (kTiles) {
-                    k = sb / sb_grid;
-                    sg = sb - k * sb_grid;
-                }
-                const uint32_t wx = ((sg % nsx) * 8u + (b & 7u)) * 8u + (w & 7u);
-                const uint32_t wy = ((sg / nsx) * 8u + (b >> 3)) * 8u + (w >> 3);
-                if (wx >= gw || wy >= gh) continue;  // padding of an edge superblock
+            }
+            for (uint32_t cur = w0; cur < w0 + chunk; ++cur) {
+                const uint32_t b = cur >> 6, w = cur & 63u;  // b = 0 in block slots
+                const uint32_t wx = sx0 + (b & 7u) * 8u + (w & 7u);
+                const uint32_t wy = sy0 + (b >> 3) * 8u + (w >> 3);
+                if (wx >= gw || wy >= gh) continue;  // padding of an edge block
                 const uint32_t olx = wx * tw, oly = wy * th;
                 uint32_t ox = olx, oy = oly;
                 if (kTiles) {
@@ -1302,7 +1344,10 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
 #ifdef RT_TIMELINE
                 // per unit {start, end, hw_id << 32 | xcc << 16 | wave index}
                 // after the 65536 per-wave records
-                const unsigned long long uid = (unsigned long long)sb * 4096u + b * 64u + w;
+                const uint32_t sbt = k * sb_grid + (wy >> 6) * nsx + (wx >> 6);
+                const unsigned long long uid = (unsigned long long)sbt * 4096u +
+                                               (((wy >> 3) & 7u) * 8u + ((wx >> 3) & 7u)) * 64u +
+                                               (wy & 7u) * 8u + (wx & 7u);
                 if (a.timeline && (threadIdx.x & 63u) == 0 && uid < (1ull << 22)) {
                     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
                     const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // XCC_ID
@@ -1514,7 +1559,8 @@ static void launch_waveq(K kernel, const FrameArgs& a, size_t lds, hipStream_t s
     // (60-65 VGPRs), but their 94 SGPRs leave room for 7: the 8th per CU
     // only starts when another exits, finds nothing and adds 8 queue atomics
     // to the tail (profiles/r02/timeline_hwid.log).  Capped at the build's
-    // waves per SIMD: C3 -0.8%, 1/8 share -5% (profiles/r02/steal_ab.log)
+    // waves per SIMD: C3 -0.8%, 1/8 share -5% (profiles/r02/steal_ab.log,
+    // measured with the static per-XCD ranges that preceded the two-level queue)
     const uint64_t cap = per_simd ? static_cast<uint64_t>(cus_of_device()) * per_simd : res;
     const uint32_t grid =
         static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(std::min<uint64_t>(res, cap), want)));

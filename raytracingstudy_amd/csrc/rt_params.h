@@ -57,7 +57,10 @@ constexpr uint32_t kCellTableOff = 0;
 constexpr uint32_t kQueueSlot = 8;
 constexpr uint32_t kWaveQueueBase = 16;
 constexpr uint32_t kWaveQueueStride = 16;
-constexpr uint32_t kCounterWords = kWaveQueueBase + 8 * kWaveQueueStride;
+// two-level wave queue: superblocks handed to XCDs (claim counter, own line)
+constexpr uint32_t kWaveQueueClaim = kWaveQueueBase + 8 * kWaveQueueStride;
+constexpr uint32_t kCounterWords = kWaveQueueClaim + 16;
+constexpr uint32_t kSlotNone = 0xFFFFFFFFu;  // slot table: no superblock left
 
 // Diagnostic build (-DRT_BLOCK_STATS, tools/block_stats.py): how many times a
 // wave executed each block of the walk (a block runs once for the wave when
@@ -93,6 +96,35 @@ inline void wave_tile_shape(uint32_t spp, uint32_t& spw, uint32_t& g, uint32_t& 
     while ((1u << lg) < ppw) ++lg;
     tw = 1u << ((lg + 1) / 2);
     th = 1u << (lg / 2);
+}
+
+// Superblocks (8x8 blocks of 8x8 wave tiles) of a scene frame's wave-tile
+// grid, or of n_tiles packed tiles.
+inline uint32_t scene_superblocks(uint32_t W, uint32_t H, uint32_t spp, uint32_t n_tiles,
+                                  uint32_t tile_size) {
+    uint32_t spw, g, ppw, tw, th;
+    wave_tile_shape(spp, spw, g, ppw, tw, th);
+    const uint32_t gw = n_tiles ? tile_size / tw : (W + tw - 1) / tw;
+    const uint32_t gh = n_tiles ? tile_size / th : (H + th - 1) / th;
+    const uint32_t nsx = ((gw + 7u) / 8u + 7u) / 8u, nsy = ((gh + 7u) / 8u + 7u) / 8u;
+    return (n_tiles ? n_tiles : 1u) * nsx * nsy;
+}
+
+// 8x8-wave-tile blocks of the same grid(s) that hold at least one wave tile.
+inline uint32_t scene_blocks(uint32_t W, uint32_t H, uint32_t spp, uint32_t n_tiles,
+                             uint32_t tile_size) {
+    uint32_t spw, g, ppw, tw, th;
+    wave_tile_shape(spp, spw, g, ppw, tw, th);
+    const uint32_t gw = n_tiles ? tile_size / tw : (W + tw - 1) / tw;
+    const uint32_t gh = n_tiles ? tile_size / th : (H + th - 1) / th;
+    return (n_tiles ? n_tiles : 1u) * ((gw + 7u) / 8u) * ((gh + 7u) / 8u);
+}
+
+// The wave queue's level-1 unit (scene_kernel): superblocks when there are
+// enough of them to balance 8 XCDs (>= 16) and they are mostly wave tiles
+// (a packed 64x64 tile below 64 spp fills 1/4 of one or less), else 8x8 blocks.
+inline uint32_t wave_queue_slot_shift(uint32_t superblocks, uint32_t blocks) {
+    return superblocks >= 16u && 4ull * blocks >= 3ull * 64u * superblocks ? 12u : 6u;
 }
 
 // Pinhole camera (include/camera.h:9-56): K and R column-major like glm.
@@ -159,6 +191,9 @@ struct FrameArgs {
     uint32_t count_work;  // 1: also count node visits / sphere tests (stats frames)
     uint32_t bts;         // block-tile side in pixels (set by the launcher)
     uint32_t wq_chunk;    // wave-queue scheduling: wave tiles per dequeue ticket (launch_scene)
+    uint32_t* wq_slots;        // two-level wave queue: per XCD, the superblock of each slot + 1
+    uint32_t wq_slot_stride;   //   (0 = not claimed yet, kSlotNone = none left); zeroed per frame
+    uint32_t wq_slot_shift;    //   slot = 2^shift wave tiles: 12 a superblock, 6 one 8x8 block
 #ifdef RT_TIMELINE
     unsigned long long* timeline;  // diagnostic build: 4 words per wave
 #endif

@@ -744,6 +744,22 @@ def test_compat_fuzz(gpu, oracle, seed):
     assert np.array_equal(img, oracle.render_compat(w, h, pose, Kr))
 
 
+@pytest.mark.parametrize("w,h,spp", [(1, 1, 64), (65, 1, 64), (577, 3, 64), (1920, 5, 64),
+                                     (300, 130, 64), (1100, 200, 64), (600, 90, 16), (97, 33, 8)])
+def test_two_level_queue_superblock_counts(gpu, oracle, w, h, spp):
+    """The wave queue's two levels (superblocks claimed by XCDs, tickets per
+    XCD over its claimed slots) at 64 spp, where a superblock is 64x64
+    pixels: 1, 2, 10, 30 (one row) and 15 superblocks, so some XCDs claim
+    none, one or several, and edge superblocks are mostly padding.  Every
+    pixel is rendered exactly once: image, radiance and counters equal the
+    oracle's, and the stats frame reports no unpublished slot.  Below 16
+    superblocks the slots are single 8x8 blocks; (1100, 200) has 18."""
+    img, rad, st, info, ref8, ref32, cnt, _ = _scene_pair(oracle, 5000, w, h, spp)
+    assert np.array_equal(img, ref8)
+    assert np.array_equal(rad, ref32)
+    _check_counts(st, cnt, 0)
+
+
 @pytest.mark.parametrize("seed", range(12))
 def test_tiles_fuzz(gpu, oracle, seed):
     """Random frame sizes, spp and tile subsets in random order through

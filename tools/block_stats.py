@@ -37,7 +37,7 @@ def main():
         fd, path = tempfile.mkstemp(suffix=".jsonl")
         os.close(fd)
         os.environ["RT_BLOCK_STATS_FILE"] = path
-        sp, al = rt.generate_spheres(c.n_spheres, rt.SEED)
+        sp, al = rt.configs.scene_spheres(c, rt.SEED)
         with rt.KernelRenderer(c.width, c.height, mode="scene", spp=c.spp, variant=args.variant) as r:
             r.resize(c.width, c.height)
             r.setPosition(scene_pose())

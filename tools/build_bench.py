@@ -31,7 +31,7 @@ def main():
     out = {}
     for name in args.configs.split(","):
         cfg = rt.CONFIGS[name]
-        sp, al = rt.generate_spheres(cfg.n_spheres, rt.SEED)
+        sp, al = rt.configs.scene_spheres(cfg, rt.SEED)
         res = {}
         trees = {}
         for hb in (False, True):

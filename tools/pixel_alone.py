@@ -50,7 +50,7 @@ def main():
     import torch
     cfg = rt.CONFIGS[args.config]
     img = full_frame_durations(args.units, cfg.width, cfg.height)
-    sp, al = rt.generate_spheres(cfg.n_spheres, rt.SEED)
+    sp, al = rt.configs.scene_spheres(cfg, rt.SEED)
     big = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=cfg.spp)
     big.resize(cfg.width, cfg.height)
     _, K = big.camera()

@@ -26,7 +26,7 @@ def main():
     args = ap.parse_args()
     import torch
     cfg = rt.CONFIGS[args.config]
-    sp, al = rt.generate_spheres(cfg.n_spheres, rt.SEED)
+    sp, al = rt.configs.scene_spheres(cfg, rt.SEED)
     r = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=cfg.spp, progressive=True)
     r.resize(cfg.width, cfg.height)
     r.setPosition(scene_pose())

@@ -31,7 +31,7 @@ def main():
     args = ap.parse_args()
     import torch
     cfg = rt.CONFIGS[args.config]
-    sp, al = rt.generate_spheres(cfg.n_spheres, rt.SEED)
+    sp, al = rt.configs.scene_spheres(cfg, rt.SEED)
     big = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=cfg.spp)
     big.resize(cfg.width, cfg.height)
     _, K = big.camera()

@@ -40,7 +40,7 @@ def main():
     for name in args.configs.split(","):
         cfg = rt.CONFIGS[name]
         spp = args.spp or cfg.spp
-        sp, al = rt.generate_spheres(cfg.n_spheres, rt.SEED)
+        sp, al = rt.configs.scene_spheres(cfg, rt.SEED)
         rs = {}
         for v in variants:
             vv, _, rest = v.partition(":")
