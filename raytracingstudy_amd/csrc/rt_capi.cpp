@@ -476,8 +476,10 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     if (stats) {
         RT_HIP(r, hipEventRecord(r->ev1, st));
         RT_HIP(r, hipEventSynchronize(r->ev1));
-        unsigned long long c[4];
-        RT_HIP(r, hipMemcpy(c, r->counters.p, sizeof(c), hipMemcpyDeviceToHost));
+        unsigned long long lines[8 * kStatLineStride], c[4] = {0, 0, 0, 0};
+        RT_HIP(r, hipMemcpy(lines, r->counters.p + kStatLineBase, sizeof(lines), hipMemcpyDeviceToHost));
+        for (uint32_t q = 0; q < 8; ++q)
+            for (uint32_t i = 0; i < 4; ++i) c[i] += lines[q * kStatLineStride + i];
         float ms = 0.f;
         RT_HIP(r, hipEventElapsedTime(&ms, r->ev0, r->ev1));
         memset(stats, 0, sizeof(*stats));

@@ -886,6 +886,11 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
     return v;
 }
 
+// Stats frames only.  Every wave adds its counts as it exits, so the adds
+// all land in the frame's tail: on ONE cache line they serialise there and
+// stall the last waves' loads behind them (plain frames that still flushed
+// were 4.3% slower on C3 and 17% on a 1/8 tile share, profiles/r02/flush_ab.log).
+// One line per XCD group cuts the queue per line 8x; the host sums the lines.
 __device__ __forceinline__ void flush_counters(const FrameArgs& a, uint32_t prim, uint32_t shadow,
                                                uint32_t nodes, uint32_t prims) {
     // ray counts are wave-uniform already (ballot counts); the work counters
@@ -895,10 +900,11 @@ __device__ __forceinline__ void flush_counters(const FrameArgs& a, uint32_t prim
     const unsigned long long s2 = wave_sum(nodes);
     const unsigned long long s3 = wave_sum(prims);
     if ((threadIdx.x & 63u) == 0) {
-        atomicAdd(a.counters + 0, s0);
-        atomicAdd(a.counters + 1, s1);
-        atomicAdd(a.counters + 2, s2);
-        atomicAdd(a.counters + 3, s3);
+        unsigned long long* c = a.counters + kStatLineBase + (blockIdx.x & 7u) * kStatLineStride;
+        atomicAdd(c + 0, s0);
+        atomicAdd(c + 1, s1);
+        atomicAdd(c + 2, s2);
+        atomicAdd(c + 3, s3);
     }
 }
 
@@ -1395,7 +1401,7 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
             }
         }
     }
-    flush_counters(a, n_primary, n_shadow, n_nodes, n_prims);
+    if (kStats) flush_counters(a, n_primary, n_shadow, n_nodes, n_prims);
 #ifdef RT_BLOCK_STATS
     if (a.bstats) {
 #pragma unroll

@@ -59,7 +59,11 @@ constexpr uint32_t kWaveQueueBase = 16;
 constexpr uint32_t kWaveQueueStride = 16;
 // two-level wave queue: superblocks handed to XCDs (claim counter, own line)
 constexpr uint32_t kWaveQueueClaim = kWaveQueueBase + 8 * kWaveQueueStride;
-constexpr uint32_t kCounterWords = kWaveQueueClaim + 16;
+// stats frames: work counters {primary, shadow, nodes, prims} per XCD group
+// (blockIdx % 8), one 128-byte line each, summed by the host
+constexpr uint32_t kStatLineBase = kWaveQueueClaim + 16;
+constexpr uint32_t kStatLineStride = 16;
+constexpr uint32_t kCounterWords = kStatLineBase + 8 * kStatLineStride;
 constexpr uint32_t kSlotNone = 0xFFFFFFFFu;  // slot table: no superblock left
 
 // Diagnostic build (-DRT_BLOCK_STATS, tools/block_stats.py): how many times a
