@@ -30,11 +30,12 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--n", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--opt", type=int, default=0, help="rt_config opt bits (A/B toggles)")
     args = ap.parse_args()
     import torch
     cfg = rt.CONFIGS[args.config]
     sp, al = rt.configs.scene_spheres(cfg, rt.SEED)
-    r = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=cfg.spp)
+    r = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=cfg.spp, opt_off=args.opt)
     r.resize(cfg.width, cfg.height)
     r.setPosition(scene_pose())
     r.set_scene(sp, al, max_depth=cfg.max_depth)
@@ -75,7 +76,7 @@ def main():
         ids = np.ascontiguousarray(ids, dtype=np.uint32)
         return timed(lambda: r.render_tiles(ids, ts, slab.data_ptr(), stream.cuda_stream))
 
-    res = {"config": args.config, "n": args.n,
+    res = {"config": args.config, "n": args.n, "opt": args.opt,
            "full_ms": timed(lambda: r.render(None, stream.cuda_stream))}
     share = T.tiles_for_rank(cfg.width, cfg.height, 0, args.n, ts)
     res["share_ms"] = tiles(share)
