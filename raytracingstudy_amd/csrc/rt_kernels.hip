@@ -1218,9 +1218,15 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
 // kMinW = minimum waves per SIMD requested from the register allocator.
 // kProg: progressive frame (a.accum set); compiled separately so plain frames
 // keep their register budget.
+// Residency of the wave-queue builds is set by SGPRs, not VGPRs: at 60-65
+// VGPRs and 94 SGPRs (112 allocated) a SIMD holds 7 waves.  The 8-wave build
+// caps its SGPRs at 80 (the rest spill into VGPR lanes, no scratch), and 8
+// waves fit: C3 -1.9%, its tile path -3.3%, C5 -2.4% (84: 8 do not fit; 76
+// and 72: the extra spills cost more; profiles/r02/sgpr_ab.log).
+// scene_kernel_w8 below is that build of the timed default.
 template <bool kTiles, uint32_t kVar, int kMinW, int kChunk, bool kStats = true,
           bool kProg = false, bool kWaveQ = false, int kLeafMode = 0>
-__global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a) {
+__device__ __forceinline__ void scene_body(FrameArgs a) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     float4* acc = lds;  // [256] running pixel sums (leader lanes' slots)
     const uint32_t wave = threadIdx.x >> 6;
@@ -1423,6 +1429,20 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
 #endif
 }
 
+template <bool kTiles, uint32_t kVar, int kMinW, int kChunk, bool kStats = true,
+          bool kProg = false, bool kWaveQ = false, int kLeafMode = 0>
+__global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a) {
+    scene_body<kTiles, kVar, kMinW, kChunk, kStats, kProg, kWaveQ, kLeafMode>(a);
+}
+
+// The timed default for spp >= 8 (variant 13, plain frames): 8 waves per SIMD,
+// SGPRs capped so that they fit (see above).
+template <bool kTiles>
+__global__ void __launch_bounds__(kBlockThreads, 8) __attribute__((amdgpu_num_sgpr(80)))
+    scene_kernel_w8(FrameArgs a) {
+    scene_body<kTiles, kVariantLaneUnified, 8, 2, false, false, true>(a);
+}
+
 __global__ void __launch_bounds__(kBlockThreads)
     unpack_kernel(const uint32_t* __restrict__ packed, const uint32_t* __restrict__ tiles,
                   uint32_t n_tiles, uint32_t ts, uint32_t tiles_x, uint32_t W, uint32_t H,
@@ -1614,14 +1634,15 @@ static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStr
                 launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false>, a,
                                   n_bt, lds, st);
             break;
-        case kVariantWaveQ:  // the spp >= 8 default: per-wave scheduling over per-XCD queues,
-            // 7 waves/SIMD (C3 -2.8%, C5 -5.4% against 6 waves, profiles/r01/occupancy_ab.log)
+        case kVariantWaveQ:  // the spp >= 8 default: per-wave scheduling over per-XCD queues.
+            // Timed (plain) frames: 8 waves/SIMD with SGPRs capped at 80
+            // (kSceneSgprs); stats frames keep 7 (their counters need the
+            // registers; C3 -2.8%, C5 -5.4% against 6, profiles/r01/occupancy_ab.log)
             if (a.count_work)
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, true, false, true>,
                              a, lds, st);
             else
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, false, false, true>,
-                             a, lds, st);
+                launch_waveq(scene_kernel_w8<kTiles>, a, lds, st, 8);
             break;
 #ifdef RT_AB_VARIANTS
         // measured-and-rejected alternatives, A/B builds only
