@@ -1287,7 +1287,7 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
         const uint32_t n1 = ks == 12u ? n_sb : (kTiles ? a.n_tiles : 1u) * nbb;  // level-1 units
         const uint32_t half = 1u << (ks - 1u);
         // the current slot's grid (packed tile) and origin in wave tiles
-        uint32_t cached_s = ~0u, k = 0, sx0 = 0, sy0 = 0;
+        uint32_t cached_s = ~0u, k = 0, sx0 = 0, sy0 = 0, tox = 0, toy = 0;
         for (;;) {
             uint32_t t = 0;
             if ((threadIdx.x & 63u) == 0) t = static_cast<uint32_t>(atomicAdd(head, 1ull));
@@ -1335,6 +1335,11 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
                     sx0 = (r % nbx) * 8u;
                     sy0 = (r / nbx) * 8u;
                 }
+                if (kTiles) {  // the packed tile's origin in the image, once per slot
+                    const uint32_t tile = a.tiles[k];
+                    tox = (tile % a.tiles_x) * a.tile_size;
+                    toy = (tile / a.tiles_x) * a.tile_size;
+                }
             }
             for (uint32_t cur = w0; cur < w0 + chunk; ++cur) {
                 const uint32_t b = cur >> 6, w = cur & 63u;  // b = 0 in block slots
@@ -1342,12 +1347,7 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
                 const uint32_t wy = sy0 + (b >> 3) * 8u + (w >> 3);
                 if (wx >= gw || wy >= gh) continue;  // padding of an edge block
                 const uint32_t olx = wx * tw, oly = wy * th;
-                uint32_t ox = olx, oy = oly;
-                if (kTiles) {
-                    const uint32_t tile = a.tiles[k];
-                    ox += (tile % a.tiles_x) * a.tile_size;
-                    oy += (tile / a.tiles_x) * a.tile_size;
-                }
+                const uint32_t ox = olx + tox, oy = oly + toy;
 #ifdef RT_TIMELINE
                 const unsigned long long tu0 = wall_clock64();
 #endif
@@ -1437,10 +1437,10 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
 
 // The timed default for spp >= 8 (variant 13, plain frames): 8 waves per SIMD,
 // SGPRs capped so that they fit (see above).
-template <bool kTiles>
+template <bool kTiles, bool kProg = false>
 __global__ void __launch_bounds__(kBlockThreads, 8) __attribute__((amdgpu_num_sgpr(80)))
     scene_kernel_w8(FrameArgs a) {
-    scene_body<kTiles, kVariantLaneUnified, 8, 2, false, false, true>(a);
+    scene_body<kTiles, kVariantLaneUnified, 8, 2, false, kProg, true>(a);
 }
 
 __global__ void __launch_bounds__(kBlockThreads)
@@ -1611,8 +1611,12 @@ static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStr
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, true, true, true>,
                              a, lds, st);
             else
+#ifdef RT_AB_PROG7  // A/B: the 7-wave progressive build (profiles/r02/tile_origin_prog8_ab.log)
                 launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, false, true, true>,
                              a, lds, st);
+#else
+                launch_waveq(scene_kernel_w8<kTiles, true>, a, lds, st, 8);
+#endif
         } else if (a.count_work) {
             launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, true>, a,
                               n_bt, lds, st);
