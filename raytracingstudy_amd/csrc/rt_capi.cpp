@@ -183,7 +183,10 @@ void fill_frame_args(rt_renderer* r, FrameArgs& a) {
     // (variant 13: C5 -15%, equal on C3, better on multi-GPU shares); 1-spp
     // frames (8x8-pixel wave tiles) keep the block-tile queue (tools/variants.py A/B,
     // profiles/r01/wave_queue_ab.log)
-    a.variant = v ? v : (a.spp >= 8u ? kVariantWaveQ : kVariantLaneUnified);
+    // spp < 8: the block-tile queue with counters only in stats frames (C2
+    // 0.185 -> 0.168 ms against the always-counting build 7,
+    // profiles/r02/c2_variant_ab.log)
+    a.variant = v ? v : (a.spp >= 8u ? kVariantWaveQ : kVariantLaneUnified2NoStats);
 }
 
 // Build the octree of the device sphere list (d_spheres) and point the

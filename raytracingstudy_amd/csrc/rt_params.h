@@ -19,7 +19,7 @@ constexpr uint32_t kVariantLane = 1;    // one ray per lane, per-thread LDS ance
 constexpr uint32_t kVariantPacket = 2;  // 64-ray wave packet, per-wave LDS stack, ballot masks
 constexpr uint32_t kVariantLaneChunk2 = 3;  // lane walk, 2 leaf spheres in flight (fewer VGPRs)
 constexpr uint32_t kVariantLaneUnified = 7;   // one walk instance for primary + shadow, 2 in flight
-constexpr uint32_t kVariantLaneUnified2NoStats = 10; // A/B: 7 with counters only in stats frames
+constexpr uint32_t kVariantLaneUnified2NoStats = 10; // spp < 8 default: 7 with counters only in stats frames
 constexpr uint32_t kVariantWaveQ = 13;     // unified walk scheduled per wave over per-XCD queues
                                            // (default for spp >= 8), 7 waves/SIMD
 constexpr uint32_t kVariantWaveQLds = 14;  // 13 + wave-uniform leaves fetched once into LDS
