@@ -1627,10 +1627,10 @@ static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStr
         return;
     }
     switch (a.variant) {
-        case kVariantLaneUnified:  // the spp < 8 default (block-tile queue)
+        case kVariantLaneUnified:  // block-tile queue, counting in every frame (A/B)
             launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2>, a, n_bt, lds, st);
             break;
-        case kVariantLaneUnified2NoStats:  // 7 with counters only in stats frames
+        case kVariantLaneUnified2NoStats:  // the spp < 8 default: 7 with counters only in stats frames
             if (a.count_work)
                 launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true>, a, n_bt,
                                   lds, st);
