@@ -1119,14 +1119,16 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
 }
 
 // Wave tile (tw x th pixels x spw samples, launch_scene) at pixel origin
-// (ox, oy); for a packed tile list also (k, olx, oly) = slot and tile-local
-// origin.  Rounds of spw samples, pairwise butterfly per round, rounds added
-// in order in the leader's LDS slot, then the mean is written.
+// (ox, oy); for a packed tile list also obase: image pixel (x, y) of this
+// tile is packed word obase + y * tile_size + x (mod 2^32; one value kept
+// live across the walks instead of the slot and the tile-local origin).
+// Rounds of spw samples, pairwise butterfly per round, rounds added in
+// order in the leader's LDS slot, then the mean is written.
 template <bool kTiles, uint32_t kVar, int kChunk, bool kStats, bool kProg, int kLeafMode>
 __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc, void* stk,
                                                 float4* lbuf,
-                                                uint32_t ox, uint32_t oy, uint32_t k,
-                                                uint32_t olx, uint32_t oly, uint32_t& n_primary,
+                                                uint32_t ox, uint32_t oy, uint32_t obase,
+                                                uint32_t& n_primary,
                                                 uint32_t& n_shadow, uint32_t& n_nodes,
                                                 uint32_t& n_prims, uint32_t* bs = nullptr) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -1189,15 +1191,13 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
         const PixelOut p{A.x * isp, A.y * isp, A.z * isp};
         const uint32_t rgba = pack_rgba8(p);
         if (kTiles) {
-            const uint32_t ts = ko->tile_size;
-            ko->out8[(size_t)k * ts * ts + (oly + qy) * ts + olx + qx] = rgba;
+            ko->out8[obase + y * ko->tile_size + x] = rgba;
         } else {
             ko->out8[(size_t)y * ko->W + x] = rgba;
             if (ko->out32) ko->out32[(size_t)y * ko->W + x] = make_float4(p.r, p.g, p.b, 1.0f);
         }
     } else if (kTiles && sub == 0 && pix < ko->ppw) {
-        const uint32_t ts = ko->tile_size;
-        ko->out8[(size_t)k * ts * ts + (oly + qy) * ts + olx + qx] = 0u;  // off-image pixel of an edge tile
+        ko->out8[obase + y * ko->tile_size + x] = 0u;  // off-image pixel of an edge tile
     }
 }
 
@@ -1287,7 +1287,7 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
         const uint32_t n1 = ks == 12u ? n_sb : (kTiles ? a.n_tiles : 1u) * nbb;  // level-1 units
         const uint32_t half = 1u << (ks - 1u);
         // the current slot's grid (packed tile) and origin in wave tiles
-        uint32_t cached_s = ~0u, k = 0, sx0 = 0, sy0 = 0, tox = 0, toy = 0;
+        uint32_t cached_s = ~0u, k = 0, sx0 = 0, sy0 = 0, tox = 0, toy = 0, obase = 0;
         for (;;) {
             uint32_t t = 0;
             if ((threadIdx.x & 63u) == 0) t = static_cast<uint32_t>(atomicAdd(head, 1ull));
@@ -1337,8 +1337,10 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
                 }
                 if (kTiles) {  // the packed tile's origin in the image, once per slot
                     const uint32_t tile = a.tiles[k];
-                    tox = (tile % a.tiles_x) * a.tile_size;
-                    toy = (tile / a.tiles_x) * a.tile_size;
+                    const uint32_t ts = a.tile_size;
+                    tox = (tile % a.tiles_x) * ts;
+                    toy = (tile / a.tiles_x) * ts;
+                    obase = k * ts * ts - toy * ts - tox;
                 }
             }
             for (uint32_t cur = w0; cur < w0 + chunk; ++cur) {
@@ -1352,7 +1354,7 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
                 const unsigned long long tu0 = wall_clock64();
 #endif
                 shade_wave_tile<kTiles, kVar, kChunk, kStats, kProg, kLeafMode>(
-                    a, acc, stk, lbuf, ox, oy, k, olx, oly, n_primary, n_shadow, n_nodes, n_prims, bs);
+                    a, acc, stk, lbuf, ox, oy, obase, n_primary, n_shadow, n_nodes, n_prims, bs);
 #ifdef RT_TIMELINE
                 // per unit {start, end, hw_id << 32 | xcc << 16 | wave index}
                 // after the 65536 per-wave records
@@ -1385,16 +1387,16 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
             __syncthreads();
             const uint32_t bt = tile_slot;
             if (bt >= n_bt) break;
-            uint32_t ox, oy, k = 0, olx = 0, oly = 0;  // block-tile origin (frame / packed tile)
+            uint32_t ox, oy, obase = 0;  // block-tile origin (frame / packed tile)
             if (kTiles) {
-                const uint32_t tpr = a.tile_size / bts;
-                k = bt / per_tile;
+                const uint32_t ts = a.tile_size, tpr = ts / bts;
+                const uint32_t k = bt / per_tile;
                 const uint32_t b = bt - k * per_tile;
-                olx = (b % tpr) * bts;
-                oly = (b / tpr) * bts;
                 const uint32_t tile = a.tiles[k];
-                ox = (tile % a.tiles_x) * a.tile_size + olx;
-                oy = (tile / a.tiles_x) * a.tile_size + oly;
+                const uint32_t tox = (tile % a.tiles_x) * ts, toy = (tile / a.tiles_x) * ts;
+                ox = tox + (b % tpr) * bts;
+                oy = toy + (b / tpr) * bts;
+                obase = k * ts * ts - toy * ts - tox;
             } else {
                 ox = (bt % bx_n) * bts;
                 oy = (bt / bx_n) * bts;
@@ -1402,8 +1404,8 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
             for (uint32_t wt = wave; wt < wtiles; wt += kBlockThreads / 64) {
                 const uint32_t wox = (wt % wtx) * tw, woy = (wt / wtx) * th;
                 shade_wave_tile<kTiles, kVar, kChunk, kStats, kProg, kLeafMode>(
-                    a, acc, stk, lbuf, ox + wox, oy + woy, k, olx + wox, oly + woy, n_primary,
-                    n_shadow, n_nodes, n_prims, bs);
+                    a, acc, stk, lbuf, ox + wox, oy + woy, obase, n_primary, n_shadow, n_nodes,
+                    n_prims, bs);
             }
         }
     }
