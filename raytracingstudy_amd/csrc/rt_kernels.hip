@@ -1273,10 +1273,12 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
         // The ticket holding the middle unit of slot s claims slot s + 1 half
         // a slot early, so waves arriving at a new slot find it published;
         // ticket 0 claims slot 0.  A claim past the last superblock publishes
-        // kSlotNone and the waves that reach it exit.  Frames of fewer than
-        // 16 superblocks claim single 8x8 blocks instead (slot = 64 units),
-        // numbered over the blocks that hold wave tiles, so a small frame
-        // spreads over all XCDs and never dequeues a superblock of padding.
+        // kSlotNone and the waves that reach it exit.  Launches of fewer
+        // than 192 superblocks (a multi-GPU tile share, small frames) claim
+        // single 8x8 blocks instead (slot = 64 units), numbered over the
+        // blocks that hold wave tiles: the XCDs then run dry within a block
+        // of each other, not within a superblock (1/8 C3 share -4%), and a
+        // small frame never dequeues a superblock of padding.
         const uint32_t q = blockIdx.x & 7u;  // this workgroup's XCD (round-robin dispatch)
         unsigned long long* head = a.counters + kWaveQueueBase + q * kWaveQueueStride;
         unsigned long long* claims = a.counters + kWaveQueueClaim;
@@ -1330,10 +1332,19 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
                     sx0 = (sg % nsx) * 64u;
                     sy0 = (sg / nsx) * 64u;
                 } else {
+                    // the grid's blocks that hold wave tiles, numbered
+                    // superblock by superblock (row-major superblocks; edge
+                    // superblocks hold vr x vc blocks)
                     k = kTiles ? g / nbb : 0u;
                     const uint32_t r = g - k * nbb;
-                    sx0 = (r % nbx) * 8u;
-                    sy0 = (r / nbx) * 8u;
+                    const uint32_t sy = r / (8u * nbx);
+                    const uint32_t vr = min(8u, nby - sy * 8u);
+                    const uint32_t r1 = r - sy * 8u * nbx;
+                    const uint32_t sx = r1 / (vr * 8u);
+                    const uint32_t vc = min(8u, nbx - sx * 8u);
+                    const uint32_t r2 = r1 - sx * vr * 8u;
+                    sx0 = (sx * 8u + r2 % vc) * 8u;
+                    sy0 = (sy * 8u + r2 / vc) * 8u;
                 }
                 if (kTiles) {  // the packed tile's origin in the image, once per slot
                     const uint32_t tile = a.tiles[k];

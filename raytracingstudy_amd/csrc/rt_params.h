@@ -125,10 +125,17 @@ inline uint32_t scene_blocks(uint32_t W, uint32_t H, uint32_t spp, uint32_t n_ti
 }
 
 // The wave queue's level-1 unit (scene_kernel): superblocks when there are
-// enough of them to balance 8 XCDs (>= 16) and they are mostly wave tiles
-// (a packed 64x64 tile below 64 spp fills 1/4 of one or less), else 8x8 blocks.
+// enough of them that one superblock is a small part of an XCD's share
+// (>= 192: C3 full frame (510), block slots cost it 0.6-3.4%; C4 8-way share
+// (255), equal within noise) and they are mostly wave
+// tiles (a packed 64x64 tile below 64 spp fills 1/4 of one or less), else
+// 8x8 blocks (1/8 and 1/4 C3 tile shares, 64 and 128: -4% and -2%,
+// profiles/r02/slot_size_ab.log).
+#ifndef RT_SLOT_SB_MIN
+#define RT_SLOT_SB_MIN 192u
+#endif
 inline uint32_t wave_queue_slot_shift(uint32_t superblocks, uint32_t blocks) {
-    return superblocks >= 16u && 4ull * blocks >= 3ull * 64u * superblocks ? 12u : 6u;
+    return superblocks >= RT_SLOT_SB_MIN && 4ull * blocks >= 3ull * 64u * superblocks ? 12u : 6u;
 }
 
 // Pinhole camera (include/camera.h:9-56): K and R column-major like glm.
