@@ -9,7 +9,13 @@ A step is one frame of the BASELINE config (default C3: 1920x1080, 64 spp,
 tiles round-robin over the ranks, each rank renders its tiles
 into a packed slab, the slabs are gathered to rank 0 over RCCL and unpacked
 into the frame there — the gather is inside the timed step.  The frame is the
-same for every N (strong scaling, BASELINE metric "at 1920x1080").
+same for every N (strong scaling, BASELINE metric "at 1920x1080").  On the
+tile path `--inflight F` (default 2) frames are in flight: frame k renders on
+stream k mod F with its own renderer (own queue heads and counters), slab and
+receive buffer, and its gather (RCCL's stream waits for that render) and
+unpack (stream k mod F waits for the gather) overlap frame k+1's render.
+Every timed frame is rendered, gathered and unpacked in full inside the
+timed region.  N=1 renders whole frames one after another on one stream.
 
 Rank 0 prints ONE JSON line.  Rays are counted by the kernel (primary + shadow
 rays actually cast) — the counts equal the CPU oracle's (tests/test_gpu_parity).
@@ -58,6 +64,10 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="process-group backend for N>1 (nccl = RCCL; gloo only to rehearse "
                          "the multi-rank path on one GPU)")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="tile path (N>1, --tiles): frames in flight, each with its own renderer, "
+                         "stream, slab and receive buffer, so frame k's gather and unpack overlap "
+                         "frame k+1's render (1 = strictly one frame after another)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal: every rank uses cuda:0 (with --backend gloo)")
     ap.add_argument("--secondary", default="c2,c5,c5d",
@@ -264,14 +274,35 @@ def main():
     _, K = r.camera()
 
     dev = torch.device("cuda", local)
+    tiled = world > 1 or args.tiles or bool(args.shard)
+    F = max(1, args.inflight) if tiled else 1
+    # frames in flight: one renderer per frame slot (the queue heads and
+    # counters are per renderer; the scene is built again, seeded the same)
+    rs = [r]
+    for _ in range(F - 1):
+        r2 = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=cfg.spp, device=local,
+                               light_dir=rt.configs.LIGHT_DIR, ambient=rt.configs.AMBIENT,
+                               variant=args.variant)
+        r2.resize(cfg.width, cfg.height)
+        r2.setPosition(pose)
+        r2.set_scene(sp, al, max_depth=cfg.max_depth, leaf_capacity=rt.configs.LEAF_CAPACITY)
+        rs.append(r2)
     # a real (non-null) stream: the kernels, the HIP events and RCCL all run on it
-    stream = torch.cuda.Stream(dev)
+    if F == 1:
+        streams = [torch.cuda.Stream(dev)]
+    else:
+        # each frame slot on its renderer's own stream: streams made one after
+        # another sit on different hardware queues, so the slots' kernels
+        # overlap (two streams from torch's pool can share a queue and then
+        # run one after the other, tools/stream_probe.py)
+        streams = [torch.cuda.ExternalStream(rr.stream_ptr(), device=dev) for rr in rs]
+    stream = streams[0]
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
     assert sptr, "need a non-null HIP stream handle"
     W, H, ts = cfg.width, cfg.height, rt.configs.TILE_SIZE
-    frame = torch.empty(W * H * 4, dtype=torch.uint8, device=dev)
-    tiled = world > 1 or args.tiles or bool(args.shard)
+    frames = [torch.empty(W * H * 4, dtype=torch.uint8, device=dev) for _ in range(F)]
+    frame = frames[0]
     if tiled:
         # tests/test_tiles_dist.py drives the same TileSharder with gloo on CPU
         if args.shard:
@@ -282,27 +313,37 @@ def main():
         else:
             sharder = TileSharder(W, H, rank, world, ts)
         my_ids = sharder.ids
-        packed = sharder.new_slab(torch, device=dev)
+        slabs = [sharder.new_slab(torch, device=dev) for _ in range(F)]
+        packed = slabs[0]
 
     events = []
 
-    def step(record: bool):
-        if record:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-        if not tiled:
-            r.render(frame.data_ptr(), sptr)
-        else:
-            r.render_tiles(my_ids, ts, packed.data_ptr(), sptr)
-        if record:
-            e1.record(stream)
-            events.append((e0, e1))
-        if tiled and not args.shard:
-            gathered = sharder.gather(packed)  # RCCL gather of the equal-size slabs to rank 0
-            # one unpack launch over all ranks' slabs (padding slots skipped)
-            sharder.unpack_fused(gathered, lambda buf, ids: r.unpack_tiles(buf.data_ptr(), ids, ts,
-                                                                          frame.data_ptr(), sptr))
+    def step(i: int, record: bool):
+        k = i % F
+        rk, sk, fk = rs[k], streams[k], frames[k]
+        skp = sk.cuda_stream
+        with torch.cuda.stream(sk):  # the collective below waits for sk's render
+            if record:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(sk)
+            if not tiled:
+                rk.render(fk.data_ptr(), skp)
+            else:
+                rk.render_tiles(my_ids, ts, slabs[k].data_ptr(), skp)
+            if record:
+                e1.record(sk)
+                events.append((e0, e1))
+            if tiled and not args.shard:
+                # RCCL gather of the equal-size slabs to rank 0, on RCCL's stream
+                gathered, work = sharder.gather(slabs[k], slot=k, async_op=True)
+                if work is not None:
+                    # sk waits for the gather: rank 0 unpacks after it, every
+                    # rank renders slot k's next frame into its slab after it
+                    work.wait()
+                # one unpack launch over all ranks' slabs (padding slots skipped)
+                sharder.unpack_fused(gathered, lambda buf, ids: rk.unpack_tiles(
+                    buf.data_ptr(), ids, ts, fk.data_ptr(), skp))
 
     # counted rays of one frame on this rank (deterministic; equal to the oracle's)
     if not tiled:
@@ -312,15 +353,15 @@ def main():
     cnt = torch.tensor([st.primary_rays, st.shadow_rays, st.nodes_visited, st.prims_tested],
                        dtype=torch.float64, device=dev)
 
-    for _ in range(args.warmup):
-        step(False)
+    for i in range(args.warmup):
+        step(i, False)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
+    for i in range(args.steps):
+        step(i, True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -344,7 +385,13 @@ def main():
         alg_bytes = float(cnt[2].item()) * NODE_BYTES + float(cnt[3].item()) * PRIM_BYTES + pix * PIXEL_BYTES
         simds = torch.cuda.get_device_properties(dev).multi_processor_count * 4
         pmc, pmc_note = load_pmc(args.pmc, cfg.name, world, rt._lib.kernel_source_id())
-        roof = roofline(kern_ms, alg_bytes, pmc if not tiled else None, simds, args.pmc, pmc_note)
+        # frames in flight overlap, so one frame's event span is not its share
+        # of the GPU: price a frame per step of wall time instead
+        roof_ms = kern_ms if F == 1 else elapsed / args.steps * 1e3
+        roof = roofline(roof_ms, alg_bytes, pmc if not tiled else None, simds, args.pmc, pmc_note)
+        roof["time_ms"] = round(roof_ms, 4)
+        roof["time_source"] = ("kernel HIP events on the launch stream" if F == 1 else
+                               f"wall time per step ({F} frames in flight)")
         roof["per_ray"] = {"nodes": float(cnt[2].item()) / float(cnt[0].item() + cnt[1].item()),
                            "prims": float(cnt[3].item()) / float(cnt[0].item() + cnt[1].item())}
         out = {
@@ -366,6 +413,7 @@ def main():
                 "octree_depth": info["max_depth"], "octree_nodes": info["n_nodes"],
                 "prim_refs": info["n_prim_refs"], "leaf_capacity": rt.configs.LEAF_CAPACITY,
                 "parallelism": f"tiles{ts}x{world}" if tiled else "single",
+                "frames_in_flight": F,
                 "rays_per_frame": int(rays_frame),
                 "primary_per_frame": int(tot[0].item()), "shadow_per_frame": int(tot[1].item()),
                 "kernel_ms": round(kern_ms, 4),
@@ -383,7 +431,7 @@ def main():
             whole = torch.empty_like(frame)
             r.render(whole.data_ptr(), sptr)
             torch.cuda.synchronize(dev)
-            out["config"]["tiles_frame_check"] = bool(torch.equal(whole, frame))
+            out["config"]["tiles_frame_check"] = all(bool(torch.equal(whole, f)) for f in frames)
         if world == 1 and not args.shard and args.secondary:
             out["secondary"] = {}
             for name in [c for c in args.secondary.split(",") if c and c != cfg.name]:
@@ -397,7 +445,8 @@ def main():
             except Exception as e:  # reported, never fatal for the GPU number
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
-    r.close()
+    for rr in rs:
+        rr.close()
     if world > 1:
         dist.destroy_process_group()
 

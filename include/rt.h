@@ -269,6 +269,11 @@ int rt_synchronize(rt_renderer* r);
 int rt_readback(rt_renderer* r, uint8_t* host_rgba8, float* host_rgba32f);
 /* Device pointer of the internal framebuffer (W*H*4 bytes). */
 void* rt_framebuffer(rt_renderer* r);
+/* The renderer's own stream (a hipStream_t made with the handle), the one a
+ * NULL stream argument means.  Extension: the reference launches on the legacy
+ * default stream (src/renderer.cu:149).  Renderers made one after another get
+ * streams on different hardware queues, so frames in flight on them overlap. */
+void* rt_stream(rt_renderer* r);
 
 /* ---- errors --------------------------------------------------------------- */
 /* Last error message for this handle (r may be NULL: last global error). */

@@ -156,6 +156,7 @@ SIGNATURES = {
     "rt_synchronize": (_int, [_P]),
     "rt_readback": (_int, [_P, _P, _P]),
     "rt_framebuffer": (_P, [_P]),
+    "rt_stream": (_P, [_P]),
     "rt_last_error": (ctypes.c_char_p, [_P]),
 }
 

@@ -983,6 +983,8 @@ int rt_readback(rt_renderer* r, uint8_t* host_rgba8, float* host_rgba32f) {
 
 void* rt_framebuffer(rt_renderer* r) { return r ? r->fb.p : nullptr; }
 
+void* rt_stream(rt_renderer* r) { return r ? static_cast<void*>(r->stream) : nullptr; }
+
 const char* rt_last_error(const rt_renderer* r) {
     if (r) return r->err.c_str();
     return g_last_error.c_str();

@@ -44,11 +44,14 @@ class TileSharder:
         dtype = dtype if dtype is not None else torch_mod.uint8
         return torch_mod.zeros(self.slab_elems, dtype=dtype, device=device)
 
-    def gather(self, slab, group=None):
+    def gather(self, slab, group=None, slot: int = 0, async_op: bool = False):
         """Equal-size gather of every rank's slab to rank 0; returns the list on rank 0.
-        The receive buffers are allocated once and reused every frame."""
+        The receive buffers are allocated once per `slot` (one per frame in
+        flight) and reused every frame.  async_op: return (list, work), where
+        work.wait() orders the caller's current stream after the collective
+        (None when nothing is left to wait for)."""
         if self.world == 1:
-            return [slab]
+            return ([slab], None) if async_op else [slab]
         import torch
         import torch.distributed as dist
         # gloo moves host tensors only: device slabs are staged through host
@@ -58,17 +61,17 @@ class TileSharder:
         out = None
         if self.rank == 0:
             key = (tuple(src.shape), src.dtype, src.device)
-            if getattr(self, "_recv_key", None) != key:
+            bufs = self.__dict__.setdefault("_recv_bufs", {})
+            if slot not in bufs or bufs[slot][0] != key:
                 # the receive slabs are views of ONE buffer (unpack_fused)
-                self._recv_buf = torch.empty((self.world,) + tuple(src.shape), dtype=src.dtype,
-                                             device=src.device)
-                self._recv = list(self._recv_buf.unbind(0))
-                self._recv_key = key
-            out = self._recv
-        dist.gather(src, out, dst=0, group=group)
+                buf = torch.empty((self.world,) + tuple(src.shape), dtype=src.dtype,
+                                  device=src.device)
+                bufs[slot] = (key, buf, list(buf.unbind(0)))
+            out = bufs[slot][2]
+        work = dist.gather(src, out, dst=0, group=group, async_op=async_op and not staged)
         if staged and out is not None:
             out = [t.to(slab.device) for t in out]
-        return out
+        return (out, work) if async_op else out
 
     def unpack_fused(self, gathered, unpack_fn: Callable[[object, np.ndarray], None]) -> None:
         """Rank 0: ONE unpack_fn(buffer, all_ids_padded) call over every rank's
@@ -77,8 +80,10 @@ class TileSharder:
         if self.rank != 0:
             return
         import torch
-        buf = getattr(self, "_recv_buf", None)
-        if buf is None or gathered[0].data_ptr() != buf.data_ptr():
+        for _, buf, _ in getattr(self, "_recv_bufs", {}).values():
+            if gathered[0].data_ptr() == buf.data_ptr():
+                break
+        else:
             buf = torch.stack(list(gathered))  # staged (gloo) slabs: make them contiguous
         unpack_fn(buf, self.all_ids_padded)
 

@@ -304,6 +304,10 @@ class KernelRenderer:
         check(self._lib.rt_readback(self._h, None, _vptr(out)), self._h)
         return out
 
+    def stream_ptr(self) -> int:
+        """The renderer's own hipStream_t (what stream=None means)."""
+        return int(self._lib.rt_stream(self._h) or 0)
+
     def framebuffer_ptr(self) -> int:
         return int(self._lib.rt_framebuffer(self._h) or 0)
 

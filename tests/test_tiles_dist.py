@@ -89,6 +89,17 @@ def _rank_main(rank, world, port, w, h, spp, q):
         sh.unpack_fused(gathered, lambda buf, ids: fused.setdefault(
             "img", T.unpack_host(buf.numpy().reshape(-1, 64, 64, 4), ids, w, h)))
         assert np.array_equal(fused["img"], per_rank)
+    # a second frame in flight (bench --inflight): its own receive buffer,
+    # the async form, the same frame
+    g1, work = sh.gather(slab, slot=1, async_op=True)
+    if work is not None:
+        work.wait()
+    if rank == 0:
+        assert g1[0].data_ptr() != gathered[0].data_ptr()
+        fused1 = {}
+        sh.unpack_fused(g1, lambda buf, ids: fused1.setdefault(
+            "img", T.unpack_host(buf.numpy().reshape(-1, 64, 64, 4), ids, w, h)))
+        assert np.array_equal(fused1["img"], per_rank)
         q.put(per_rank)
     dist.barrier()
     dist.destroy_process_group()
