@@ -645,6 +645,47 @@ def test_fused_unpack_with_padding_slots(gpu):
             r.render_tiles(np.array([rt._lib.RT_TILE_SKIP], np.uint32), ts, buf.data_ptr())
 
 
+def test_frames_in_flight_on_renderer_streams(gpu, oracle):
+    """bench.py --inflight: frames alternate over two renderers, each on its
+    own stream (rt_stream, not torch's), with no host wait between frames, so
+    their kernels overlap; every slot's slabs, unpacked by the fused unpack on
+    the slot's stream, give the oracle's frame byte for byte."""
+    import torch
+    from raytracingstudy_amd.dist import TileSharder
+    w, h, ts, world, spp, F = 300, 200, 64, 3, 64, 2
+    sp, al = rt.generate_spheres(20000, rt.SEED)
+    shards = [TileSharder(w, h, k, world, ts) for k in range(world)]
+    n = shards[0].slab_tiles
+    rs, bufs, imgs = [], [], []
+    try:
+        for _ in range(F):
+            r = rt.KernelRenderer(w, h, mode="scene", spp=spp)
+            r.resize(w, h)
+            r.setPosition(scene_pose())
+            r.set_scene(sp, al)
+            rs.append(r)
+            bufs.append(torch.zeros(world * n * ts * ts * 4, dtype=torch.uint8, device="cuda"))
+            imgs.append(torch.zeros(w * h * 4, dtype=torch.uint8, device="cuda"))
+        streams = [r.stream_ptr() for r in rs]
+        assert all(streams) and len(set(streams)) == F
+        _, K = rs[0].camera()
+        torch.cuda.synchronize()
+        for i in range(6):  # three frames per slot, back to back
+            k = i % F
+            for s, sh in enumerate(shards):
+                rs[k].render_tiles(sh.ids, ts, bufs[k].data_ptr() + s * n * ts * ts * 4, streams[k])
+            rs[k].unpack_tiles(bufs[k].data_ptr(), shards[0].all_ids_padded, ts, imgs[k].data_ptr(),
+                               streams[k])
+        for r in rs:
+            r.synchronize()
+        ref8, _, _ = oracle.Scene(sp, al).render(w, h, scene_pose(), K, spp=spp, radiance=False)
+        for img in imgs:
+            assert np.array_equal(img.cpu().numpy().reshape(h, w, 4), ref8)
+    finally:
+        for r in rs:
+            r.close()
+
+
 def _fuzz_case(seed: int):
     """One seeded random scene / camera / render setting (test_scene_fuzz)."""
     g = np.random.default_rng(seed)
