@@ -272,46 +272,42 @@ def test_frames_on_two_caller_streams_are_ordered(gpu, oracle):
         int(c) for c in cnt)
 
 
-def test_scene_c4_rows(gpu, oracle):
-    """C4 (3840x2160, 64 spp, 100k spheres), every 16th row from row 7
-    (135 rows = 1/16 of the frame)."""
-    img, rad, st, info, ref8, ref32, cnt, _ = _scene_pair(oracle, 100_000, 3840, 2160, 64,
-                                                           row_step=16, row_phase=7)
-    rows = np.arange(7, 2160, 16)
-    assert len(rows) == 135
-    assert np.array_equal(img[rows], ref8[rows])
-    assert np.array_equal(rad[rows], ref32[rows])
+def test_scene_c4_full_frame(gpu, oracle):
+    """C4 (3840x2160, 64 spp, 100k spheres) over the whole frame (all 2160
+    rows): RGBA8 and radiance bit-exact, all four counters equal."""
+    img, rad, st, info, ref8, ref32, cnt, _ = _scene_pair(oracle, 100_000, 3840, 2160, 64)
+    assert np.array_equal(img, ref8)
+    assert np.array_equal(rad, ref32)
     assert st.primary_rays == 3840 * 2160 * 64
+    _check_counts(st, cnt, 0)
 
 
-def test_scene_c5_rows(gpu, oracle):
-    """C5 (1920x1080, 256 spp, 1M spheres, depth-12 octree), every 16th row from
-    row 5 (68 rows, 1/16 of the frame)."""
+def test_scene_c5_full_frame(gpu, oracle):
+    """C5 (1920x1080, 256 spp, 1M spheres, depth-12 octree) over the whole
+    frame: RGBA8 and radiance bit-exact, all four counters equal."""
     img, rad, st, info, ref8, ref32, cnt, oinfo = _scene_pair(oracle, 1_000_000, 1920, 1080, 256,
-                                                               depth=12, row_step=16, row_phase=5)
+                                                               depth=12)
     assert (info["n_nodes"], info["n_prim_refs"]) == (oinfo["n_nodes"], oinfo["n_prim_refs"])
     assert info["cell_table_depth"] == 6
-    rows = np.arange(5, 1080, 16)
-    assert np.array_equal(img[rows], ref8[rows])
-    assert np.array_equal(rad[rows], ref32[rows])
+    assert np.array_equal(img, ref8)
+    assert np.array_equal(rad, ref32)
+    _check_counts(st, cnt, 0)
 
 
-def test_scene_c5_deep_rows(gpu, oracle):
+def test_scene_c5_deep_full_frame(gpu, oracle):
     """C5d: 1M clustered spheres whose octree reaches depth 12 (BASELINE config
     5's "deep (depth-12) octree"; walk depths 9-12 and the cell table at scale),
-    1920x1080, 256 spp, every 16th row from row 3 (68 rows, 1/16 of the
-    frame) bit-exact; the resolution-driven depth limit is src/renderer.cu:134-136's."""
+    1920x1080, 256 spp, the whole frame bit-exact and all four counters equal;
+    the resolution-driven depth limit is src/renderer.cu:134-136's."""
     c = rt.CONFIGS["c5d"]
     sp, al = rt.configs.scene_spheres(c)
     img, rad, st, info, ref8, ref32, cnt, oinfo = _scene_pair(
-        oracle, c.n_spheres, c.width, c.height, c.spp, depth=c.max_depth, row_step=16,
-        row_phase=3, spheres=(sp, al))
+        oracle, c.n_spheres, c.width, c.height, c.spp, depth=c.max_depth, spheres=(sp, al))
     assert info["depth_reached"] == oinfo["depth_reached"] == 12
     assert (info["n_nodes"], info["n_prim_refs"]) == (oinfo["n_nodes"], oinfo["n_prim_refs"])
-    rows = np.arange(3, c.height, 16)
-    assert len(rows) == 68
-    assert np.array_equal(img[rows], ref8[rows])
-    assert np.array_equal(rad[rows], ref32[rows])
+    assert np.array_equal(img, ref8)
+    assert np.array_equal(rad, ref32)
+    _check_counts(st, cnt, 0)
 
 
 def test_c4_eight_rank_tile_plan(gpu):
