@@ -471,9 +471,15 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         // cnt >= 1 (a leaf is a non-empty cell; the root leaf is guarded by
         // its caller): a do-while skips the loop-entry test and its branch
         uint32_t j = 0;
+        // Slot q of a chunk holds one of the leaf's spheres iff j + q < cnt.
+        // Slot 0 always does (j < cnt inside the do-while), and for q >= 1
+        // the test is j < cnt - q against a per-leaf bound: no per-chunk
+        // m = cnt - j, no second loop counter and no mask for slot 0.
+        const auto in_leaf = [&](int q) -> bool {
+            return q == 0 || static_cast<int>(j) < static_cast<int>(cnt) - q;
+        };
         do {
             RT_BS(kBsLeafChunk);
-            const uint32_t m = cnt - j;
             // kChunk unconditional dwordx4 loads in flight at fixed offsets; a
             // slot past the leaf's end reads the next leaf or the array's
             // kPrimPad tail (in bounds) and is never tested
@@ -496,7 +502,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 // unconditional (a slot past the leaf's end holds a real
                 // sphere record too), masked without a branch
                 const bool pos = !(isect_h(o0, o1, o2, d0, d1, d2, sv[q]) < 0.0f);
-                maybe |= (m > static_cast<uint32_t>(q)) & pos;
+                maybe |= in_leaf(q) & pos;
             }
             // marked unlikely (it is: most chunks pass no lane): the exact
             // tests are laid out off the fall-through path (C3 -0.6%, C5
@@ -504,9 +510,9 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             if (__builtin_expect(__any(maybe), 0)) {
 #pragma unroll
                 for (int q = 0; q < kChunk; ++q)
-                    if (m > static_cast<uint32_t>(q) && test(sv[q], off + j + q)) return true;
+                    if (in_leaf(q) && test(sv[q], off + j + q)) return true;
             } else if (kStats) {
-                n_prims += min(m, static_cast<uint32_t>(kChunk));
+                n_prims += min(cnt - j, static_cast<uint32_t>(kChunk));
             }
             j += kChunk;
         } while (j < cnt);
