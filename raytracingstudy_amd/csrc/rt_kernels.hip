@@ -499,10 +499,12 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             bool maybe = false;
 #pragma unroll
             for (int q = 0; q < kChunk; ++q) {
-                // unconditional (a slot past the leaf's end holds a real
-                // sphere record too), masked without a branch
+                // unconditional and unmasked: a slot past the leaf's end holds
+                // a real sphere record too, and if it passes the screen the
+                // exact tests below still skip it (in_leaf), so it can only
+                // send the chunk down the exact path for nothing
                 const bool pos = !(isect_h(o0, o1, o2, d0, d1, d2, sv[q]) < 0.0f);
-                maybe |= in_leaf(q) & pos;
+                maybe |= pos;
             }
             // marked unlikely (it is: most chunks pass no lane): the exact
             // tests are laid out off the fall-through path (C3 -0.6%, C5
