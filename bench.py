@@ -200,9 +200,12 @@ def roofline(kern_ms: float, touched_bytes: float, pmc, simds: int, pmc_path: st
     return out
 
 
-def secondary_config(rt, torch, name: str, dev, stream, steps: int = 3) -> dict:
+def secondary_config(rt, torch, name: str, dev, stream, steps: int = 3, pmc_path: str = "",
+                     simds: int = 1024) -> dict:
     """Time another BASELINE config on this GPU: kernel ms (HIP events on the
-    launch stream), Mrays/s from the counted rays, scene build time."""
+    launch stream), Mrays/s from the counted rays, scene build time, and its
+    roofline when the PMC summary holds this config at this build's kernel
+    sources (profiles/pmc_latest.json, key = config name)."""
     import numpy as np
     from raytracingstudy_amd.camera import scene_pose
 
@@ -225,7 +228,15 @@ def secondary_config(rt, torch, name: str, dev, stream, steps: int = 3) -> dict:
             e1.synchronize()
             ms.append(e0.elapsed_time(e1))
         k = float(np.median(ms))
-        return {"workload": f"{c.width}x{c.height}, {c.spp} spp, {c.n_spheres} {c.scene} spheres, "
+        alg = (st.nodes_visited * NODE_BYTES + st.prims_tested * PRIM_BYTES +
+               c.width * c.height * PIXEL_BYTES)
+        pmc, note = load_pmc(pmc_path, name, 1, rt._lib.kernel_source_id()) if pmc_path else (None, "")
+        roof = roofline(k, alg, pmc, simds, pmc_path, note)
+        roof["time_ms"] = round(k, 4)
+        roof["per_ray"] = {"nodes": st.nodes_visited / rays, "prims": st.prims_tested / rays}
+        if pmc and pmc.get("valu_lane_util") is not None:
+            roof["valu_lane_util"] = round(pmc["valu_lane_util"], 4)
+        return {"roofline": roof, "workload": f"{c.width}x{c.height}, {c.spp} spp, {c.n_spheres} {c.scene} spheres, "
                             f"max depth {info['max_depth']}",
                 "depth_reached": info["depth_reached"], "cell_table_depth": info["cell_table_depth"],
                 "kernel_ms": round(k, 3), "Mrays_s": round(rays / k / 1e3, 1),
@@ -389,6 +400,8 @@ def main():
         # of the GPU: price a frame per step of wall time instead
         roof_ms = kern_ms if F == 1 else elapsed / args.steps * 1e3
         roof = roofline(roof_ms, alg_bytes, pmc if not tiled else None, simds, args.pmc, pmc_note)
+        if pmc and pmc.get("valu_lane_util") is not None and not tiled:
+            roof["valu_lane_util"] = round(pmc["valu_lane_util"], 4)
         roof["time_ms"] = round(roof_ms, 4)
         roof["time_source"] = ("kernel HIP events on the launch stream" if F == 1 else
                                f"wall time per step ({F} frames in flight)")
@@ -416,7 +429,11 @@ def main():
                 "frames_in_flight": F,
                 "rays_per_frame": int(rays_frame),
                 "primary_per_frame": int(tot[0].item()), "shadow_per_frame": int(tot[1].item()),
-                "kernel_ms": round(kern_ms, 4),
+                # with frames in flight a frame's event span overlaps the
+                # other slots' kernels: it is reported as a span, not a kernel time
+                "kernel_ms": round(kern_ms, 4) if F == 1 else None,
+                "render_span_ms": round(kern_ms, 4),
+                "wall_ms_per_step": round(elapsed / args.steps * 1e3, 4),
                 "scene_build_ms": round(info["build_ms"], 1),
                 "scene_upload_ms": round(info["upload_ms"], 1),
             },
@@ -437,7 +454,8 @@ def main():
             out["secondary"] = {}
             for name in [c for c in args.secondary.split(",") if c and c != cfg.name]:
                 try:
-                    out["secondary"][name] = secondary_config(rt, torch, name, dev, stream)
+                    out["secondary"][name] = secondary_config(rt, torch, name, dev, stream,
+                                                              pmc_path=args.pmc, simds=simds)
                 except Exception as e:  # reported, never fatal for the headline
                     out["secondary"][name] = {"error": repr(e)}
         if world == 1 and args.cpu_baseline == "auto":

@@ -85,6 +85,10 @@ enum {
     RT_FLAG_COMPAT_FMA = 1u << 6,  /* compat mode: evaluate getRay (include/camera.h:31-34) with
                                       the FMA contraction nvcc's default -fmad=true applies to
                                       the reference binary; off = source order */
+    /* bits 8..9, test-only: what fills the padding after the last leaf list
+     * (DESIGN.md §4): 0 zero spheres (default), 1 NaN spheres, 2 spheres
+     * covering the root box.  Images and counters are the same for all three. */
+    RT_FLAG_PAD_FILL_SHIFT = 8,
     /* bits 16..19: scene-kernel variant for A/B runs (0 = default: 13, the
      * per-wave queue, for spp >= 8, else 7; others in DESIGN.md 5.1); images
      * and counters are identical across variants (packets: images only) */

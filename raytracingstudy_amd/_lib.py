@@ -35,12 +35,12 @@ RT_FLAG_COMPAT_FMA = 1 << 6
 RT_BUILDER_DEVICE = 0
 RT_BUILDER_HOST = 1
 RT_TILE_SKIP = 0xFFFFFFFF  # rt_unpack_tiles: a padding slot, not copied
+RT_FLAG_PAD_FILL_SHIFT = 8  # test-only: 0 zeros, 1 NaN, 2 covering spheres after the last leaf
 RT_FLAG_VARIANT_SHIFT = 16
 RT_FLAG_OPT_SHIFT = 20
 RT_FLAG_CELL_TABLE_SHIFT = 28
 RT_CELL_TABLE_OFF = 15
-VARIANT_LANE = 1    # one ray per lane, separate primary/shadow walks (A/B)
-VARIANT_PACKET = 2  # 64-ray wave packets (A/B)
+VARIANT_REMOVED = 2  # a removed variant number (the packet walk): rt_create refuses it
 VARIANT_BLOCK = 7   # unified walk, block-tile queue (default for spp < 8)
 VARIANT_WAVEQ = 13  # unified walk, per-wave per-XCD queues (default for spp >= 8)
 

@@ -59,6 +59,9 @@ struct rt_renderer {
     hipEvent_t done = nullptr;
     hipStream_t last_stream = nullptr;
     bool pending = false;
+    // the last frame ran on the wave queue: rt_synchronize / rt_readback check
+    // its 'slot never published' flag (stats frames check it themselves)
+    bool check_queue = false;
     float pose[16];
     float K[9];
     uint32_t W = 0, H = 0;
@@ -284,6 +287,32 @@ int build_scene(rt_renderer* r) {
         memcpy(rmax, tree.rmax, sizeof(rmax));
     }
     {
+        // The kPrimPad tail after the last leaf list is read by the leaf loads
+        // (a chunk's slot past the end of the LAST leaf) and joins the leaf
+        // screen unmasked; its tests are skipped, so only time could depend on
+        // it.  Neither builder writes it: fill it here so that nothing a frame
+        // does depends on what the allocation held before.  Zero spheres
+        // (r = 0) by default; the test-only fill modes put spheres there that
+        // pass the screen (NaN, or one covering the root box) to prove the
+        // images and counters do not depend on the tail.
+        const uint32_t mode = (r->cfg.flags >> RT_FLAG_PAD_FILL_SHIFT) & 3u;
+        float4 pad[kPrimPad];
+        for (uint32_t i = 0; i < kPrimPad; ++i) {
+            if (mode == 1) {
+                pad[i] = make_float4(NAN, NAN, NAN, NAN);
+            } else if (mode == 2) {
+                const float c = 0.5f * (rmin[0] + rmax[0]);
+                pad[i] = make_float4(c, 0.5f * (rmin[1] + rmax[1]), 0.5f * (rmin[2] + rmax[2]),
+                                     4.0f * (rmax[0] - rmin[0] + rmax[1] - rmin[1] + rmax[2] - rmin[2]));
+            } else {
+                pad[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+        float4* tail = const_cast<float4*>(sc.prim_sp) + in.n_prim_refs;
+        RT_HIP(r, hipMemcpyAsync(tail, pad, sizeof(pad), hipMemcpyHostToDevice, r->stream));
+        RT_HIP(r, hipStreamSynchronize(r->stream));
+    }
+    {
         // depth-K cell table over the tree (flags bits 28..31: 0 auto, 15 off, else K)
         const uint32_t f = (r->cfg.flags >> RT_FLAG_CELL_TABLE_SHIFT) & 0xFu;
         const uint32_t k_req = f == 0 ? kCellTableAuto : f == 15 ? kCellTableOff : f;
@@ -464,6 +493,7 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     }
 #endif
     if ((ost = mark_queued(r, st))) return ost;
+    r->check_queue = a.wq_slots != nullptr && !stats;
 #ifdef RT_TIMELINE
     if (tl_file) {
         std::vector<unsigned long long> h(tl_words);
@@ -562,8 +592,10 @@ int rt_create(const rt_config* cfg, rt_renderer** out) {
         return fail(nullptr, RT_E_INVALID, "rt_create: unknown mode");
     if (!variant_available((cfg->flags >> RT_FLAG_VARIANT_SHIFT) & 0xFu))
         return fail(nullptr, RT_E_INVALID,
-                    "rt_create: scene-kernel variant not in this build (A/B variants need the "
-                    "-DRT_AB_VARIANTS library, make ab)");
+                    "rt_create: scene-kernel variant not in this build (0, 7, 10 or 13)");
+    if (((cfg->flags >> (RT_FLAG_OPT_SHIFT + kOptChunkShift)) & 7u) > kOptChunkMax)
+        return fail(nullptr, RT_E_INVALID,
+                    "rt_create: wave-queue ticket size field (flags bits 24..26) must be 0..4");
     rt_renderer* r = new (std::nothrow) rt_renderer();
     if (!r) return fail(nullptr, RT_E_NOMEM, "rt_create: out of host memory");
     r->cfg = *cfg;
@@ -955,13 +987,27 @@ int rt_reset_accumulation(rt_renderer* r) {
     return RT_OK;
 }
 
+// After the renderer's work has completed: the wave queue's bounded wait
+// (rt_kernels.hip) flags a frame whose slot was never published instead of
+// hanging; report it for the last frame.
+static int check_last_frame(rt_renderer* r) {
+    if (!r->check_queue) return RT_OK;
+    r->check_queue = false;
+    unsigned long long qerr = 0;
+    RT_HIP(r, hipMemcpy(&qerr, r->counters.p + kWaveQueueClaim + 1, sizeof(qerr),
+                        hipMemcpyDeviceToHost));
+    if (qerr)
+        return fail(r, RT_E_HIP, "scene kernel: wave-queue slot never published (frame incomplete)");
+    return RT_OK;
+}
+
 int rt_synchronize(rt_renderer* r) {
     if (!r) return RT_E_INVALID;
     int st;
     if ((st = set_device(r))) return st;
     RT_HIP(r, hipStreamSynchronize(r->stream));
     if (r->pending) RT_HIP(r, hipEventSynchronize(r->done));
-    return RT_OK;
+    return check_last_frame(r);
 }
 
 int rt_readback(rt_renderer* r, uint8_t* host_rgba8, float* host_rgba32f) {
@@ -971,6 +1017,7 @@ int rt_readback(rt_renderer* r, uint8_t* host_rgba8, float* host_rgba32f) {
     // the frame may have been queued on a caller's stream
     RT_HIP(r, hipStreamSynchronize(r->stream));
     if (r->pending) RT_HIP(r, hipEventSynchronize(r->done));
+    if ((st = check_last_frame(r))) return st;
     const size_t px = (size_t)r->W * r->H;
     if (host_rgba8) RT_HIP(r, hipMemcpy(host_rgba8, r->fb.p, px * 4, hipMemcpyDeviceToHost));
     if (host_rgba32f) {

@@ -177,24 +177,6 @@ __device__ __forceinline__ float readlane_f(float x, uint32_t lane) {
     return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(x), lane));
 }
 
-// Ray bundle of one walk phase (DESIGN.md 5.1 "Bundle prefilter"): the wave's
-// rays lie within A (origins) and B (unit directions) of a reference ray
-// (o, d) taken from one of its lanes.  For a sphere (c, r) with perpendicular
-// distance D* from the reference line, every lane's line is at least
-// D* - A - (|c - o| + A) B away, and |c - o| <= |b| + D* (b = (c - o).d), so
-// no lane's discriminant can be >= 0 unless
-//     D* <= R = (r + eps + A + (|b| + A) B) / (1 - B),   B <= 1/2,
-// evaluated as (r + c0 + |b| c1) * c2 with 1/(1 - B) <= 1 + 2B.  eps =
-// kBundleEps (1 + |b| + A) is orders of magnitude above the float error of
-// both the lanes' h and this test.  Spheres failing it are skipped for the
-// whole wave; the others get the lanes' exact isect, in list order.
-constexpr float kBundleEps = 1.0f / 16384.0f;
-struct Bundle {
-    float o0, o1, o2, d0, d1, d2;
-    float c0, c1, c2;  // c0 = eps (1 + A) + A + A B, c1 = eps + B, c2 = 1 + 2B
-    bool ok;           // false: per-lane leaf tests (non-finite or too wide bundle)
-};
-
 // isect's discriminant h alone (same operations): h < 0 <=> isect rejects
 // the sphere before its square root.
 __device__ __forceinline__ float isect_h(float o0, float o1, float o2, float d0, float d1,
@@ -225,15 +207,12 @@ __host__ __device__ inline uint32_t stack_levels(const SceneArgs& S) {
 // The per-thread ancestor stack lives in LDS, [depth-1][thread] (conflict-free).
 // kAnyHit: compile-time any-hit; with kDynAny the mode comes from `any_rt`
 // instead, so ONE inlined walk serves both the primary and the shadow ray.
-template <bool kAnyHitT, int kChunk = 4, bool kDynAny = false, bool kStats = true,
-          bool kLdsLeaf = false, bool kSmemLeaf = false, bool kLaneLeaf = false,
-          bool kBundle = false>
+template <bool kAnyHitT, int kChunk = 2, bool kDynAny = false, bool kStats = true>
 __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, float o2, float d0,
                                      float d1, float d2, float tmin, float tmax, float& tout,
                                      uint32_t& iout, uint32_t& n_nodes, uint32_t& n_prims,
                                      uint2* __restrict__ stk, bool any_rt = false,
-                                     float4* __restrict__ lbuf = nullptr, uint32_t* bs = nullptr,
-                                     const Bundle* bun = nullptr) {
+                                     uint32_t* bs = nullptr) {
     const bool kAnyHit = kDynAny ? any_rt : kAnyHitT;
     const uint32_t D = S.max_depth;
     const uint32_t G = 1u << D;
@@ -295,176 +274,8 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         return false;
     };
     // Leaf spheres in list order (same order, hence same counters, as the
-    // oracle): each lane loads its own, kChunk loads in flight.  kLdsLeaf /
-    // kSmemLeaf / kLaneLeaf are measured alternatives for wave-uniform leaves
-    // (variants 14-16), none faster.
-    // Bundle-prefiltered leaf (kBundle): the lanes in this block share out the
-    // leaf's spheres (lane of rank k loads sphere k), test each against the
-    // wave's ray bundle, and only the spheres some lane could hit are then
-    // tested exactly by every lane of the leaf, in list order.  Lanes in other
-    // leaves are served leaf by leaf (first pending lane's leaf first).  Same
-    // spheres accepted, same order, same results as the per-lane loop below.
-    auto leaf_bundle = [&](uint32_t off, uint32_t cnt) -> bool {
-        bool pending = true, found = false;
-        for (;;) {
-            const uint64_t pm = __ballot(pending);
-            if (pm == 0) break;
-            const uint32_t lead = static_cast<uint32_t>(__builtin_ctzll(pm));
-            const uint32_t uoff = __builtin_amdgcn_readlane(off, lead);
-            const uint32_t ucnt = __builtin_amdgcn_readlane(cnt, lead);
-            const bool mine = pending && off == uoff;
-            RT_BS(kBsLeaf);
-            const uint64_t ex = __ballot(1);
-            const uint32_t nact = static_cast<uint32_t>(__popcll(ex));
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-                static_cast<uint32_t>(ex >> 32),
-                __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(ex), 0u));
-            uint32_t hit_at = ucnt;  // list position of this lane's any-hit
-            for (uint32_t base = 0; base < ucnt; base += nact) {
-                RT_BS(kBsLeafChunk);
-                const uint32_t j = base + rank;
-                float4 sp;  // lanes past the leaf's end never become candidates
-                bool pass = false;
-                if (j < ucnt) {
-                    sp = prim_sp[uoff + j];
-                    const float ox = sp.x - bun->o0, oy = sp.y - bun->o1, oz = sp.z - bun->o2;
-                    const float b = fmaf(oz, bun->d2, fmaf(oy, bun->d1, ox * bun->d0));
-                    const float qx = fmaf(-b, bun->d0, ox);
-                    const float qy = fmaf(-b, bun->d1, oy);
-                    const float qz = fmaf(-b, bun->d2, oz);
-                    const float qq = fmaf(qz, qz, fmaf(qy, qy, qx * qx));
-                    const float R = fmaf(fabsf(b), bun->c1, sp.w + bun->c0) * bun->c2;
-                    pass = qq <= R * R;
-                }
-                uint64_t cm = __ballot(pass);
-                while (cm) {
-                    const uint32_t L = static_cast<uint32_t>(__builtin_ctzll(cm));
-                    cm &= cm - 1u;
-                    float4 c;
-                    c.x = readlane_f(sp.x, L);
-                    c.y = readlane_f(sp.y, L);
-                    c.z = readlane_f(sp.z, L);
-                    c.w = readlane_f(sp.w, L);
-                    const uint32_t jj =
-                        base + static_cast<uint32_t>(__popcll(ex & ((1ull << L) - 1ull)));
-                    if (mine && !found) {
-                        RT_BS(kBsTest);
-                        float th;
-                        if (isect(o0, o1, o2, d0, d1, d2, c, tmin, tmax, th, bs)) {
-                            RT_BS(kBsAccept);
-                            const uint32_t ref = uoff + jj;
-                            if (kAnyHit) {
-                                tout = th;
-                                found = true;
-                                hit_at = jj;
-                            } else if (th < best_t) {
-                                best_t = th;
-                                best_ref = ref;
-                            } else if (th == best_t && S.prim_idx[ref] < S.prim_idx[best_ref]) {
-                                best_ref = ref;
-                            }
-                        }
-                    }
-                }
-            }
-            // counters as the per-lane loop counts them: every sphere of the
-            // leaf, or up to and including an any-hit
-            if (kStats && mine) n_prims += found ? hit_at + 1u : ucnt;
-            pending = pending && !mine;
-        }
-        return found;
-    };
+    // oracle): each lane loads its own, kChunk loads in flight.
     auto leaf = [&](uint32_t off, uint32_t cnt) -> bool {
-        // wave-uniform leaves only: lanes in different leaves are served
-        // concurrently by the per-lane loop below (one latency for all)
-        if (kBundle && bun->ok && __all(off == __builtin_amdgcn_readfirstlane(off)))
-            return leaf_bundle(off, cnt);
-#ifdef RT_AB_VARIANTS
-        if (kLdsLeaf) {
-            // Wave-uniform leaf (the usual case: the lanes are one pixel's
-            // samples): the active lanes fetch the leaf's spheres once, one
-            // sphere per lane, into the wave's LDS buffer, and every lane then
-            // reads them by LDS broadcast.  A wave-wide dwordx4 load returns
-            // 1 KB through the texture-data path per sphere, which PMC shows
-            // ~96% busy; this returns 16 B per sphere.  Same spheres, same
-            // order, same tests as the vector path below.
-            const uint32_t uoff = __builtin_amdgcn_readfirstlane(off);
-            const uint32_t ucnt = __builtin_amdgcn_readfirstlane(cnt);
-            if (ucnt <= kLeafBuf && __all(off == uoff)) {
-                const uint64_t act = __ballot(1);
-                const uint32_t n_act = static_cast<uint32_t>(__popcll(act));
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-                    static_cast<uint32_t>(act >> 32),
-                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(act), 0u));
-                for (uint32_t i = rank; i < ucnt; i += n_act) lbuf[i] = prim_sp[uoff + i];
-                // one wave's LDS operations complete in order: no barrier needed
-                for (uint32_t j = 0; j < ucnt; j += 2) {
-                    const float4 s0 = lbuf[j];
-                    const float4 s1 = lbuf[min(j + 1u, ucnt - 1u)];
-                    if (test(s0, uoff + j)) return true;
-                    if (j + 1u < ucnt && test(s1, uoff + j + 1u)) return true;
-                }
-                return false;
-            }
-        }
-        if (kLaneLeaf) {
-            // Wave-uniform leaf: only the first active lane loads each sphere
-            // (a one-lane vector load: L1-cached like the wave-wide one, a
-            // fraction of its address/data-path cycles) and readfirstlane
-            // broadcasts it into SGPRs for every lane's test.
-            const uint32_t uoff = __builtin_amdgcn_readfirstlane(off);
-            const uint32_t ucnt = __builtin_amdgcn_readfirstlane(cnt);
-            if (__all(off == uoff)) {
-                const uint32_t lane_id = __lane_id();
-                const float4* __restrict__ ps = prim_sp + uoff;
-                for (uint32_t j = 0; j < ucnt; j += 2) {
-                    // the loader is the first lane still testing (any-hit lanes
-                    // leave the loop as soon as they hit)
-                    const uint32_t first = __builtin_amdgcn_readfirstlane(lane_id);
-                    float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
-                    if (lane_id == first) {
-                        a0 = ps[j];
-                        a1 = ps[min(j + 1u, ucnt - 1u)];
-                    }
-                    float4 b0, b1;
-                    b0.x = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a0.x)));
-                    b0.y = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a0.y)));
-                    b0.z = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a0.z)));
-                    b0.w = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a0.w)));
-                    b1.x = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a1.x)));
-                    b1.y = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a1.y)));
-                    b1.z = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a1.z)));
-                    b1.w = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(a1.w)));
-                    if (test(b0, uoff + j)) return true;
-                    if (j + 1u < ucnt && test(b1, uoff + j + 1u)) return true;
-                }
-                return false;
-            }
-        }
-        if (kSmemLeaf) {
-            // Wave-uniform leaf read by the SCALAR unit: 4 spheres (64 B) per
-            // scalar load straight into SGPRs, which the sphere tests take as
-            // operands.  Nothing is written into 64 lanes' VGPRs (a wave-wide
-            // dwordx4 load writes 1 KB of VGPRs per sphere).  Reads past the
-            // leaf end stay inside the arrays' 4-sphere padding.
-            const uint32_t uoff = __builtin_amdgcn_readfirstlane(off);
-            const uint32_t ucnt = __builtin_amdgcn_readfirstlane(cnt);
-            if (__all(off == uoff)) {
-                const float4* __restrict__ ps = prim_sp + uoff;
-                for (uint32_t j = 0; j < ucnt; j += 4) {
-                    float4 sv[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) sv[q] = ps[j + q];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        if (j + q < ucnt && test(sv[q], uoff + j + q)) return true;
-                }
-                return false;
-            }
-        }
-#else
-        static_assert(!kLdsLeaf && !kSmemLeaf && !kLaneLeaf, "leaf modes are A/B builds (-DRT_AB_VARIANTS)");
-#endif
         const float4* __restrict__ ps = prim_sp + off;
         static_assert(kChunk <= kPrimPad + 1, "leaf loads may run kChunk-1 spheres past a leaf");
         RT_BS(kBsLeaf);
@@ -678,202 +489,6 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
     return false;
 }
 
-#ifdef RT_AB_VARIANTS
-// ---------------------------------------------------------------------------
-// Packet variant: the wave walks the octree as ONE 64-ray packet.
-//
-// An 8x8 pixel block's jittered primary rays are coherent, and all shadow
-// rays share the light direction, so the union of the cells the 64 rays cross
-// is close to one ray's.  The wave therefore keeps ONE traversal stack (in
-// LDS, per wave) of (node record, cell, 64-bit lane mask) entries:
-//   * children of an internal node are culled per lane with the same grid
-//     plane formula as walk<> (entry/exit of every child from 9 planes) and
-//     pushed far-to-near (front-to-back for the majority mirror octant) with
-//     their __ballot lane mask; empty masks are never pushed;
-//   * a popped entry re-checks its lanes against best_t (nearest) / done
-//     (any-hit); a zero mask skips the node for the whole wave;
-//   * node records and sphere records are read at wave-uniform addresses
-//     (scalar loads, broadcast) and each sphere is tested by all active lanes.
-// Per-lane results are the nearest (t, index) over every sphere whose cells
-// the ray crosses — the same definition the oracle's walk computes (order-
-// independent: ties go to the smaller index), so images are bit-identical.
-// Counters: nodes = lane-node visits, prims = lane-sphere tests (work done).
-// ---------------------------------------------------------------------------
-
-struct PStackEntry {
-    uint32_t rx, ry;   // node record
-    uint32_t c01;      // c0 | c1 << 16   (REAL grid coordinates at `depth`)
-    uint32_t c2dl;     // c2 | depth << 16 | leaf << 24
-    uint32_t mlo, mhi; // lane mask
-    uint32_t pad0, pad1;
-};
-
-__device__ __forceinline__ uint32_t ufirst(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-
-template <bool kAnyHit>
-__device__ __forceinline__ bool walk_packet(const SceneArgs& S, bool want, float o0, float o1,
-                                            float o2, float d0, float d1, float d2, float tmin,
-                                            float& tout, uint32_t& iout, uint32_t& n_nodes,
-                                            uint32_t& n_prims, PStackEntry* __restrict__ stk) {
-    const uint32_t G = 1u << S.max_depth;
-    const float o[3] = {o0, o1, o2};
-    const float d[3] = {d0, d1, d2};
-    float inv[3], nog[3];
-    bool mir[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const float g = (o[i] - S.rmin[i]) * S.scale[i];
-        mir[i] = d[i] < 0.0f;
-        float a = fabsf(d[i]);
-        if (a < 1e-20f) a = 1e-20f;
-        const float og = mir[i] ? S.G - g : g;
-        inv[i] = 1.0f / (a * S.scale[i]);
-        nog[i] = -(og * inv[i]);
-    }
-    auto plane_m = [&](int i, uint32_t km) { return fmaf(static_cast<float>(km), inv[i], nog[i]); };
-    // t of the plane at REAL grid coordinate k, in this lane's mirrored frame
-    auto P = [&](int i, uint32_t k) { return plane_m(i, mir[i] ? G - k : k); };
-    float t0 = plane_m(0, 0), t1 = plane_m(0, G);
-#pragma unroll
-    for (int i = 1; i < 3; ++i) {
-        const float a0 = plane_m(i, 0), a1 = plane_m(i, G);
-        if (a0 > t0) t0 = a0;
-        if (a1 < t1) t1 = a1;
-    }
-    if (t0 < tmin) t0 = tmin;
-    bool on = want && (t0 < t1);
-    float best_t = INFINITY;
-    uint32_t best = kNoHit;
-    bool done = false;
-    const uint64_t m0 = __ballot(on);
-    if (m0 == 0) return false;
-    n_nodes += on ? 1u : 0u;
-
-    // majority mirror octant -> front-to-back child order for the packet
-    const uint32_t pop = __popcll(m0);
-    uint32_t rm = 0;
-    if (2u * __popcll(__ballot(on && mir[0])) > pop) rm |= 1u;
-    if (2u * __popcll(__ballot(on && mir[1])) > pop) rm |= 2u;
-    if (2u * __popcll(__ballot(on && mir[2])) > pop) rm |= 4u;
-
-    const float4* __restrict__ prim_sp = S.prim_sp;
-    const uint32_t* __restrict__ prim_idx = S.prim_idx;
-    const uint2* __restrict__ nodes = S.nodes;
-    const uint32_t lane = __lane_id();
-
-    auto do_leaf = [&](uint32_t off, uint32_t cnt, bool lane_on) {
-        for (uint32_t j = 0; j < cnt; ++j) {
-            const float4 sp = prim_sp[off + j];
-            const uint32_t idx = kAnyHit ? 0u : prim_idx[off + j];
-            if (lane_on) {
-                n_prims += 1;
-                float th;
-                if (isect(o0, o1, o2, d0, d1, d2, sp, tmin, INFINITY, th)) {
-                    if (kAnyHit) {
-                        done = true;
-                        lane_on = false;
-                        tout = th;
-                    } else if (th < best_t || (th == best_t && idx < best)) {
-                        best_t = th;
-                        best = idx;
-                    }
-                }
-            }
-            if (kAnyHit && __ballot(lane_on) == 0) break;
-        }
-    };
-
-    int top = 0;
-    auto expand = [&](uint32_t depth, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t rx,
-                      uint32_t ry, bool lane_on) {
-        const uint32_t h = G >> (depth + 1);
-        const uint32_t cc[3] = {c0, c1, c2};
-        float E0[3], X0[3], E1[3], X1[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const uint32_t lo = cc[i] * 2u * h;
-            const float pl = P(i, lo), pm = P(i, lo + h), ph = P(i, lo + 2u * h);
-            E0[i] = mir[i] ? pm : pl;
-            X0[i] = mir[i] ? pl : pm;
-            E1[i] = mir[i] ? ph : pm;
-            X1[i] = mir[i] ? pm : ph;
-        }
-        const uint32_t valid = ry & 0xFFu, leafm = (ry >> 8) & 0xFFu;
-        // push far -> near: order {0,1,2,4,3,5,6,7} ^ rm is front-to-back
-        const uint32_t ord[8] = {7, 6, 5, 3, 4, 2, 1, 0};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const uint32_t ch = ord[k] ^ rm;
-            if (!((valid >> ch) & 1u)) continue;
-            const uint32_t b0 = ch & 1u, b1 = (ch >> 1) & 1u, b2 = ch >> 2;
-            float te = fmaxf(fmaxf(b0 ? E1[0] : E0[0], b1 ? E1[1] : E0[1]), b2 ? E1[2] : E0[2]);
-            float tx = fminf(fminf(b0 ? X1[0] : X0[0], b1 ? X1[1] : X0[1]), b2 ? X1[2] : X0[2]);
-            te = te < tmin ? tmin : te;
-            tx = tx > t1 ? t1 : tx;
-            const bool ok = lane_on && te <= tx && (kAnyHit ? !done : te <= best_t);
-            const uint64_t mk = __ballot(ok);
-            if (mk == 0) continue;
-            const uint32_t slot = rx + __builtin_popcount(valid & ((1u << ch) - 1u));
-            const uint2 crec = nodes[slot];
-            if (lane == 0) {
-                PStackEntry e;
-                e.rx = crec.x;
-                e.ry = crec.y;
-                e.c01 = (2u * c0 + b0) | ((2u * c1 + b1) << 16);
-                e.c2dl = (2u * c2 + b2) | ((depth + 1u) << 16) | (((leafm >> ch) & 1u) << 24);
-                e.mlo = static_cast<uint32_t>(mk);
-                e.mhi = static_cast<uint32_t>(mk >> 32);
-                e.pad0 = e.pad1 = 0;
-                stk[top] = e;
-            }
-            ++top;
-        }
-    };
-
-    if (S.root_is_leaf) {
-        do_leaf(S.root.x, S.root.y, on);
-    } else {
-        expand(0, 0, 0, 0, S.root.x, S.root.y, on);
-        while (top > 0) {
-            --top;
-            const PStackEntry e = stk[top];
-            const uint32_t rx = ufirst(e.rx), ry = ufirst(e.ry);
-            const uint32_t c01 = ufirst(e.c01), c2dl = ufirst(e.c2dl);
-            const uint64_t mk = (static_cast<uint64_t>(ufirst(e.mhi)) << 32) | ufirst(e.mlo);
-            const uint32_t c0 = c01 & 0xFFFFu, c1 = c01 >> 16, c2 = c2dl & 0xFFFFu;
-            const uint32_t depth = (c2dl >> 16) & 0xFFu;
-            const bool leaf = (c2dl >> 24) & 1u;
-            bool lane_on = (mk >> lane) & 1u;
-            if (kAnyHit) {
-                lane_on = lane_on && !done;
-            } else if (lane_on) {
-                const uint32_t size = G >> depth;
-                const float e0 = P(0, mir[0] ? (c0 + 1u) * size : c0 * size);
-                const float e1 = P(1, mir[1] ? (c1 + 1u) * size : c1 * size);
-                const float e2 = P(2, mir[2] ? (c2 + 1u) * size : c2 * size);
-                float te = fmaxf(fmaxf(e0, e1), e2);
-                te = te < tmin ? tmin : te;
-                lane_on = te <= best_t;
-            }
-            if (__ballot(lane_on) == 0) continue;
-            n_nodes += lane_on ? 1u : 0u;
-            if (leaf)
-                do_leaf(rx, ry, lane_on);
-            else
-                expand(depth, c0, c1, c2, rx, ry, lane_on);
-            if (kAnyHit && __ballot(on && !done) == 0) break;
-        }
-    }
-    if (kAnyHit) return done;
-    if (best != kNoHit) {
-        tout = best_t;
-        iout = best;
-        return true;
-    }
-    return false;
-}
-#endif  // RT_AB_VARIANTS (packet walk)
-
 // ---------------------------------------------------------------------------
 // Frame mapping, shading, ordered accumulation
 //
@@ -927,119 +542,6 @@ __device__ __forceinline__ void flush_counters(const FrameArgs& a, uint32_t prim
     }
 }
 
-#ifdef RT_AB_VARIANTS
-// One sample of pixel (x, y): primary walk, Lambert shade, shadow walk.
-// kVar selects the traversal; `valid` lanes trace, the others only take part
-// in the packet walks' wave-wide votes.
-template <uint32_t kVar, int kChunk>
-__device__ __forceinline__ PixelOut sample_color(const FrameArgs& a, uint32_t x, uint32_t y,
-                                                 uint32_t hp, uint32_t s, bool valid,
-                                                 uint32_t& n_shadow, uint32_t& n_nodes,
-                                                 uint32_t& n_prims, void* stk) {
-    const SceneArgs& S = a.sc;
-    float u = static_cast<float>(x), v = static_cast<float>(y);
-    if (a.jitter) {
-        u = u + u01(mix32(hp ^ (s << 1)));
-        v = v + u01(mix32(hp ^ ((s << 1) | 1u)));
-    }
-    float d0, d1, d2;
-    get_ray(a.cam, u, v, d0, d1, d2);
-    float t = 0.0f;
-    uint32_t idx = 0;
-    bool hit = false;
-    if (kVar == kVariantPacket) {
-        hit = walk_packet<false>(S, valid, a.cam.o[0], a.cam.o[1], a.cam.o[2], d0, d1, d2, 0.0f, t,
-                                 idx, n_nodes, n_prims, static_cast<PStackEntry*>(stk));
-    } else if (valid) {
-        hit = walk<false, kChunk>(S, a.cam.o[0], a.cam.o[1], a.cam.o[2], d0, d1, d2, 0.0f, INFINITY,
-                                  t, idx, n_nodes, n_prims, static_cast<uint2*>(stk));
-    }
-    const float miss_r = 200.0f / 255.0f;
-    PixelOut c{miss_r, sat(d1), sat(d2)};
-    float p0 = 0.f, p1 = 0.f, p2 = 0.f, n0 = 0.f, n1 = 0.f, n2 = 0.f, lam = 0.f;
-    uint32_t al = 0;
-    bool want_shadow = false;
-    if (hit) {
-        const float4 sp = S.spheres[idx];
-        p0 = a.cam.o[0] + t * d0;
-        p1 = a.cam.o[1] + t * d1;
-        p2 = a.cam.o[2] + t * d2;
-        const float ir = 1.0f / sp.w;
-        n0 = (p0 - sp.x) * ir;
-        n1 = (p1 - sp.y) * ir;
-        n2 = (p2 - sp.z) * ir;
-        const float ndl = n0 * a.L[0] + n1 * a.L[1] + n2 * a.L[2];
-        lam = ndl > 0.0f ? ndl : 0.0f;
-        want_shadow = ndl > 0.0f && a.shadows;
-        al = S.albedo[idx];
-    }
-    const float s0 = p0 + n0 * kShadowEps, s1 = p1 + n1 * kShadowEps, s2 = p2 + n2 * kShadowEps;
-    float ts;
-    uint32_t is;
-    // ray counters are wave-uniform (SGPRs): lanes that cast, counted by ballot
-    n_shadow += static_cast<uint32_t>(__popcll(__ballot(want_shadow)));
-    if (kVar == kVariantPacket) {
-        if (__ballot(want_shadow)) {
-            if (walk_packet<true>(S, want_shadow, s0, s1, s2, a.L[0], a.L[1], a.L[2], 0.0f, ts, is,
-                                  n_nodes, n_prims, static_cast<PStackEntry*>(stk)))
-                lam = 0.0f;
-        }
-    } else if (want_shadow) {
-        if (walk<true, kChunk>(S, s0, s1, s2, a.L[0], a.L[1], a.L[2], 0.0f, INFINITY, ts, is,
-                               n_nodes, n_prims, static_cast<uint2*>(stk)))
-            lam = 0.0f;
-    }
-    if (hit) {
-        const float f = a.ambient + (1.0f - a.ambient) * lam;
-        c.r = static_cast<float>(al & 0xFFu) * (1.0f / 255.0f) * f;
-        c.g = static_cast<float>((al >> 8) & 0xFFu) * (1.0f / 255.0f) * f;
-        c.b = static_cast<float>((al >> 16) & 0xFFu) * (1.0f / 255.0f) * f;
-    }
-    return c;
-}
-#endif  // RT_AB_VARIANTS (separate primary/shadow walks)
-
-// The bundle of the rays `active` lanes are about to walk (converged code:
-// every lane of the wave executes this).  Reference = the first active lane's
-// ray; A, B = the largest origin / direction distance from it.
-__device__ __forceinline__ void make_bundle(Bundle& bn, bool active, float o0, float o1, float o2,
-                                            float d0, float d1, float d2) {
-    const uint64_t am = __ballot(active);
-    bn.ok = false;
-    if (am == 0) return;
-    const uint32_t f = static_cast<uint32_t>(__builtin_ctzll(am));
-    bn.o0 = readlane_f(o0, f);
-    bn.o1 = readlane_f(o1, f);
-    bn.o2 = readlane_f(o2, f);
-    bn.d0 = readlane_f(d0, f);
-    bn.d1 = readlane_f(d1, f);
-    bn.d2 = readlane_f(d2, f);
-    float ea = 0.0f, eb = 0.0f;
-    if (active) {
-        const float x = o0 - bn.o0, y = o1 - bn.o1, z = o2 - bn.o2;
-        const float u = d0 - bn.d0, v = d1 - bn.d1, w = d2 - bn.d2;
-        ea = fmaf(z, z, fmaf(y, y, x * x));
-        eb = fmaf(w, w, fmaf(v, v, u * u));
-    }
-    // a non-finite lane (or reference) disables the prefilter for the walk
-    const bool bad = active && !(ea <= 3.0e38f && eb <= 3.0e38f &&
-                                 fabsf(o0) <= 3.0e38f && fabsf(o1) <= 3.0e38f && fabsf(o2) <= 3.0e38f);
-#pragma unroll
-    for (int m = 32; m > 0; m >>= 1) {
-        ea = fmaxf(ea, __shfl_xor(ea, m, 64));
-        eb = fmaxf(eb, __shfl_xor(eb, m, 64));
-    }
-    if (__any(bad)) return;
-    // every lane holds the maxima now: make them wave-uniform (SGPRs)
-    const float A = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(sqrtf(ea))));
-    const float B = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(sqrtf(eb))));
-    if (!(B <= 0.5f) || !(A <= 1.0e30f)) return;
-    bn.c0 = fmaf(kBundleEps, 1.0f + A, A + A * B);
-    bn.c1 = kBundleEps + B;
-    bn.c2 = 1.0f + 2.0f * B;
-    bn.ok = true;
-}
-
 // The kernel's FrameArgs as memory (the kernarg segment, scalar-cached),
 // behind an opaque pointer: a field read through it is a fresh s_load at that
 // point instead of a value kept live in an SGPR across the walk (the register
@@ -1054,15 +556,12 @@ __device__ __forceinline__ KernArgs* kernargs() {
 
 // Unified lane path: one walk instance run twice (primary, then the shadow ray
 // of the lanes that need one), so the register allocator sees one walk.
-// kLeafMode: 0 vector loads, 1 LDS-staged uniform leaves, 2 scalar-loaded uniform
-// leaves, 3 one-lane loads + readfirstlane broadcast for uniform leaves
-template <int kChunk, bool kStats, int kLeafMode = 0>
+template <int kChunk, bool kStats>
 __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uint32_t x,
                                                          uint32_t y, uint32_t hp, uint32_t s,
                                                          bool valid, uint32_t& n_shadow,
                                                          uint32_t& n_nodes, uint32_t& n_prims,
-                                                         void* stk, float4* lbuf = nullptr,
-                                                         uint32_t* bs = nullptr) {
+                                                         void* stk, uint32_t* bs = nullptr) {
     const SceneArgs& S = a.sc;
     KernArgs* ka = kernargs();
     float u = static_cast<float>(x), v = static_cast<float>(y);
@@ -1085,14 +584,11 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
         float t = 0.0f;
         uint32_t idx = 0;
         bool hit = false;
-        Bundle bun;
-        if (kLeafMode == 4) make_bundle(bun, active, r0, r1, r2, d0, d1, d2);
         if (active) {
             RT_BS(kBsPhase);
-            hit = walk<false, kChunk, true, kStats, kLeafMode == 1, kLeafMode == 2,
-                       kLeafMode == 3, kLeafMode == 4>(
-                S, r0, r1, r2, d0, d1, d2, 0.0f, INFINITY, t, idx, n_nodes, n_prims,
-                static_cast<uint2*>(stk), any, lbuf, bs, &bun);
+            hit = walk<false, kChunk, true, kStats>(S, r0, r1, r2, d0, d1, d2, 0.0f, INFINITY, t,
+                                                    idx, n_nodes, n_prims,
+                                                    static_cast<uint2*>(stk), any, bs);
         }
         if (phase == 0) {
             hit0 = active && hit;
@@ -1143,9 +639,8 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
 // live across the walks instead of the slot and the tile-local origin).
 // Rounds of spw samples, pairwise butterfly per round, rounds added in
 // order in the leader's LDS slot, then the mean is written.
-template <bool kTiles, uint32_t kVar, int kChunk, bool kStats, bool kProg, int kLeafMode>
+template <bool kTiles, int kChunk, bool kStats, bool kProg>
 __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc, void* stk,
-                                                float4* lbuf,
                                                 uint32_t ox, uint32_t oy, uint32_t obase,
                                                 uint32_t& n_primary,
                                                 uint32_t& n_shadow, uint32_t& n_nodes,
@@ -1171,17 +666,8 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
         const uint32_t sg = r * spw + sub_base;
         const bool valid = lane_ok && sg < s_end;
         n_primary += static_cast<uint32_t>(__popcll(__ballot(valid)));  // wave-uniform
-#ifdef RT_AB_VARIANTS
-        PixelOut c = kVar == kVariantLaneUnified
-                         ? sample_color_unified<kChunk, kStats, kLeafMode>(
-                               a, x, y, hp, sg, valid, n_shadow, n_nodes, n_prims, stk, lbuf, bs)
-                         : sample_color<kVar, kChunk>(a, x, y, hp, sg, valid, n_shadow,
-                                                            n_nodes, n_prims, stk);
-#else
-        static_assert(kVar == kVariantLaneUnified, "other walks are A/B builds (-DRT_AB_VARIANTS)");
-        PixelOut c = sample_color_unified<kChunk, kStats, kLeafMode>(
-            a, x, y, hp, sg, valid, n_shadow, n_nodes, n_prims, stk, lbuf, bs);
-#endif
+        PixelOut c = sample_color_unified<kChunk, kStats>(a, x, y, hp, sg, valid, n_shadow,
+                                                          n_nodes, n_prims, stk, bs);
         // Pixel sum of this round: pairwise butterfly over the pixel's g
         // lanes (missing samples are 0) = oracle.c:tree_sum; rounds are then
         // added in order in the leader's LDS slot.
@@ -1243,22 +729,12 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
 // waves fit: C3 -1.9%, its tile path -3.3%, C5 -2.4% (84: 8 do not fit; 76
 // and 72: the extra spills cost more; profiles/r02/sgpr_ab.log).
 // scene_kernel_w8 below is that build of the timed default.
-template <bool kTiles, uint32_t kVar, int kMinW, int kChunk, bool kStats = true,
-          bool kProg = false, bool kWaveQ = false, int kLeafMode = 0>
+template <bool kTiles, int kChunk, bool kStats = true, bool kProg = false, bool kWaveQ = false>
 __device__ __forceinline__ void scene_body(FrameArgs a) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     float4* acc = lds;  // [256] running pixel sums (leader lanes' slots)
     const uint32_t wave = threadIdx.x >> 6;
     void* stk = reinterpret_cast<uint2*>(lds + kBlockThreads) + threadIdx.x;
-#ifdef RT_AB_VARIANTS
-    if (kVar == kVariantPacket)
-        stk = reinterpret_cast<PStackEntry*>(lds + kBlockThreads) + wave * a.stack_entries;
-#endif
-    // per-wave leaf buffer after the ancestor stacks (scene_lds_bytes)
-    float4* lbuf = nullptr;
-    if (kLeafMode == 1) {
-        lbuf = lds + kBlockThreads + stack_levels(a.sc) * (kBlockThreads / 2) + wave * kLeafBuf;
-    }
     const uint32_t tw = a.tw, th = a.th;
     uint32_t n_shadow = 0, n_nodes = 0, n_prims = 0, n_primary = 0;
 #ifdef RT_BLOCK_STATS
@@ -1383,8 +859,8 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
 #ifdef RT_TIMELINE
                 const unsigned long long tu0 = wall_clock64();
 #endif
-                shade_wave_tile<kTiles, kVar, kChunk, kStats, kProg, kLeafMode>(
-                    a, acc, stk, lbuf, ox, oy, obase, n_primary, n_shadow, n_nodes, n_prims, bs);
+                shade_wave_tile<kTiles, kChunk, kStats, kProg>(
+                    a, acc, stk, ox, oy, obase, n_primary, n_shadow, n_nodes, n_prims, bs);
 #ifdef RT_TIMELINE
                 // per unit {start, end, hw_id << 32 | xcc << 16 | wave index}
                 // after the 65536 per-wave records
@@ -1433,8 +909,8 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
             }
             for (uint32_t wt = wave; wt < wtiles; wt += kBlockThreads / 64) {
                 const uint32_t wox = (wt % wtx) * tw, woy = (wt / wtx) * th;
-                shade_wave_tile<kTiles, kVar, kChunk, kStats, kProg, kLeafMode>(
-                    a, acc, stk, lbuf, ox + wox, oy + woy, obase, n_primary, n_shadow, n_nodes,
+                shade_wave_tile<kTiles, kChunk, kStats, kProg>(
+                    a, acc, stk, ox + wox, oy + woy, obase, n_primary, n_shadow, n_nodes,
                     n_prims, bs);
             }
         }
@@ -1461,10 +937,10 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
 #endif
 }
 
-template <bool kTiles, uint32_t kVar, int kMinW, int kChunk, bool kStats = true,
-          bool kProg = false, bool kWaveQ = false, int kLeafMode = 0>
+template <bool kTiles, int kMinW, int kChunk, bool kStats = true, bool kProg = false,
+          bool kWaveQ = false>
 __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a) {
-    scene_body<kTiles, kVar, kMinW, kChunk, kStats, kProg, kWaveQ, kLeafMode>(a);
+    scene_body<kTiles, kChunk, kStats, kProg, kWaveQ>(a);
 }
 
 // The timed default for spp >= 8 (variant 13, plain frames): 8 waves per SIMD,
@@ -1472,7 +948,7 @@ __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a
 template <bool kTiles, bool kProg = false>
 __global__ void __launch_bounds__(kBlockThreads, 8) __attribute__((amdgpu_num_sgpr(80)))
     scene_kernel_w8(FrameArgs a) {
-    scene_body<kTiles, kVariantLaneUnified, 8, 2, false, kProg, true>(a);
+    scene_body<kTiles, 2, false, kProg, true>(a);
 }
 
 __global__ void __launch_bounds__(kBlockThreads)
@@ -1509,15 +985,8 @@ hipError_t launch_compat(const FrameArgs& a, hipStream_t st) {
 
 size_t scene_lds_bytes(const FrameArgs& a) {
     const size_t colours = kBlockThreads * sizeof(float4);  // pixel sums
-#ifdef RT_AB_VARIANTS
-    if (a.variant == kVariantPacket)
-        return colours + static_cast<size_t>(a.stack_entries) * (kBlockThreads / 64) * sizeof(PStackEntry);
-#endif
     const uint32_t levels = stack_levels(a.sc);
-    const size_t leafbuf = a.variant == kVariantWaveQLds
-                               ? static_cast<size_t>(kBlockThreads / 64) * kLeafBuf * sizeof(float4)
-                               : 0;
-    return colours + static_cast<size_t>(levels) * kBlockThreads * sizeof(uint2) + leafbuf;
+    return colours + static_cast<size_t>(levels) * kBlockThreads * sizeof(uint2);
 }
 
 // Resident workgroups on the device for a kernel at a given LDS size.  The
@@ -1637,125 +1106,50 @@ static void launch_waveq(K kernel, const FrameArgs& a, size_t lds, hipStream_t s
 
 template <bool kTiles>
 static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStream_t st) {
-    if (a.accum) {  // progressive frames: the unified walk, whatever the A/B variant
-        if (a.spp >= 8u) {  // 7 waves/SIMD like variant 13 (no spills since the uniform counters)
+    if (a.accum) {  // progressive frames: the unified walk, whatever the variant
+        if (a.spp >= 8u) {  // the wave queue, like variant 13
             if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, true, true, true>,
-                             a, lds, st);
+                launch_waveq(scene_kernel<kTiles, 7, 2, true, true, true>, a, lds, st);
             else
-#ifdef RT_AB_PROG7  // A/B: the 7-wave progressive build (profiles/r02/tile_origin_prog8_ab.log)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, false, true, true>,
-                             a, lds, st);
-#else
                 launch_waveq(scene_kernel_w8<kTiles, true>, a, lds, st, 8);
-#endif
         } else if (a.count_work) {
-            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, true>, a,
-                              n_bt, lds, st);
+            launch_persistent(scene_kernel<kTiles, 1, 2, true, true>, a, n_bt, lds, st);
         } else {
-            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, true>, a,
-                              n_bt, lds, st);
+            launch_persistent(scene_kernel<kTiles, 1, 2, false, true>, a, n_bt, lds, st);
         }
         return;
     }
     switch (a.variant) {
-        case kVariantLaneUnified:  // block-tile queue, counting in every frame (A/B)
-            launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2>, a, n_bt, lds, st);
+        case kVariantLaneUnified:  // block-tile queue, counting in every frame
+            launch_persistent(scene_kernel<kTiles, 1, 2>, a, n_bt, lds, st);
             break;
         case kVariantLaneUnified2NoStats:  // the spp < 8 default: 7 with counters only in stats frames
             if (a.count_work)
-                launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true>, a, n_bt,
-                                  lds, st);
+                launch_persistent(scene_kernel<kTiles, 1, 2, true>, a, n_bt, lds, st);
             else
-                launch_persistent(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false>, a,
-                                  n_bt, lds, st);
+                launch_persistent(scene_kernel<kTiles, 1, 2, false>, a, n_bt, lds, st);
             break;
         case kVariantWaveQ:  // the spp >= 8 default: per-wave scheduling over per-XCD queues.
             // Timed (plain) frames: 8 waves/SIMD with SGPRs capped at 80
             // (kSceneSgprs); stats frames keep 7 (their counters need the
             // registers; C3 -2.8%, C5 -5.4% against 6, profiles/r01/occupancy_ab.log)
             if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, true, false, true>,
-                             a, lds, st);
+                launch_waveq(scene_kernel<kTiles, 7, 2, true, false, true>, a, lds, st);
             else
                 launch_waveq(scene_kernel_w8<kTiles>, a, lds, st, 8);
             break;
-#ifdef RT_AB_VARIANTS
-        // measured-and-rejected alternatives, A/B builds only
-        case kVariantWaveQBundle:  // 13 + bundle-prefiltered leaves
-            if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, true, false, true, 4>,
-                             a, lds, st);
-            else
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 7, 2, false, false, true, 4>,
-                             a, lds, st);
-            break;
-        case kVariantPacket:
-            launch_persistent(scene_kernel<kTiles, kVariantPacket, 1, 4>, a, n_bt, lds, st);
-            break;
-        case kVariantLaneChunk2:
-            launch_persistent(scene_kernel<kTiles, kVariantLane, 1, 2>, a, n_bt, lds, st);
-            break;
-        case kVariantLane:
-            launch_persistent(scene_kernel<kTiles, kVariantLane, 1, 4>, a, n_bt, lds, st);
-            break;
-        case kVariantWaveQLds:  // 13 + wave-uniform leaves staged through LDS
-            if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true, 1>,
-                             a, lds, st, 0);
-            else
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true, 1>,
-                             a, lds, st, 0);
-            break;
-        case kVariantWaveQLane:  // 13 + one-lane loads broadcast by readfirstlane
-            if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true, 3>,
-                             a, lds, st, 0);
-            else
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true, 3>,
-                             a, lds, st, 0);
-            break;
-        case kVariantWaveQSmem:  // 13 + wave-uniform leaves read by scalar loads
-            if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true, 2>,
-                             a, lds, st, 0);
-            else
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true, 2>,
-                             a, lds, st, 0);
-            break;
-        case kVariantWaveQ6:  // 13 at the allocator's own occupancy (6 waves/SIMD)
-            if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, true, false, true>,
-                             a, lds, st, 0);
-            else
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 1, 2, false, false, true>,
-                             a, lds, st, 0);
-            break;
-        case kVariantWaveQ8:  // 13 compiled for 8 waves/SIMD
-            if (a.count_work)
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 8, 2, true, false, true>,
-                             a, lds, st, 8);
-            else
-                launch_waveq(scene_kernel<kTiles, kVariantLaneUnified, 8, 2, false, false, true>,
-                             a, lds, st, 8);
-            break;
-#endif
         default:  // rejected by variant_available() before any launch
             break;
     }
 }
 
-// Variants compiled into this build (rt_create refuses the others).
+// Variants compiled into this build (rt_create refuses the others).  The
+// measured-and-rejected alternatives of DESIGN.md 5.1 (packets, LDS / scalar /
+// one-lane uniform leaves, bundle prefilter, 6- and 8-wave builds) were
+// removed in round 3; their A/B logs stay under profiles/.
 bool variant_available(uint32_t v) {
-    if (v == 0 || v == kVariantLaneUnified || v == kVariantLaneUnified2NoStats || v == kVariantWaveQ)
-        return true;
-#ifdef RT_AB_VARIANTS
-    return v == kVariantLane || v == kVariantPacket || v == kVariantLaneChunk2 ||
-           v == kVariantWaveQLds || v == kVariantWaveQSmem || v == kVariantWaveQLane ||
-           v == kVariantWaveQ6 || v == kVariantWaveQ8 || v == kVariantWaveQBundle;
-#else
-    return false;
-#endif
+    return v == 0 || v == kVariantLaneUnified || v == kVariantLaneUnified2NoStats ||
+           v == kVariantWaveQ;
 }
 
 hipError_t launch_scene(const FrameArgs& a_in, hipStream_t st) {
@@ -1770,7 +1164,6 @@ hipError_t launch_scene(const FrameArgs& a_in, hipStream_t st) {
     // 1 per ticket, more is slower; profiles/r01/chunk_ab.log)
     const uint32_t ck = (a.sc.opt >> kOptChunkShift) & 7u;
     a.wq_chunk = ck ? 1u << (ck - 1u) : std::max(1u, 4u / std::max(1u, std::min(a.rounds, 4u)));
-    a.stack_entries = 8u * a.sc.max_depth + 8u;
     const size_t lds = scene_lds_bytes(a);
     if (a.tiles)
         launch_scene_t<true>(a, 0, lds, st);

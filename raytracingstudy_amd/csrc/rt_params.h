@@ -14,22 +14,16 @@ constexpr uint32_t kMaxDepth = 16;  // octree depth limit (grid coordinates stay
 constexpr float kShadowEps = 1e-5f; // shadow-ray origin offset along the normal (world units)
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 
-// scene kernel variants (rt_config.flags bits 16..19, RT_FLAG_VARIANT_SHIFT)
-constexpr uint32_t kVariantLane = 1;    // one ray per lane, per-thread LDS ancestor stack
-constexpr uint32_t kVariantPacket = 2;  // 64-ray wave packet, per-wave LDS stack, ballot masks
-constexpr uint32_t kVariantLaneChunk2 = 3;  // lane walk, 2 leaf spheres in flight (fewer VGPRs)
+// scene kernel variants (rt_config.flags bits 16..19, RT_FLAG_VARIANT_SHIFT);
+// 0 picks 13 for spp >= 8, else 10.  Numbers of the variants measured and
+// removed are not reused.
 constexpr uint32_t kVariantLaneUnified = 7;   // one walk instance for primary + shadow, 2 in flight
 constexpr uint32_t kVariantLaneUnified2NoStats = 10; // spp < 8 default: 7 with counters only in stats frames
 constexpr uint32_t kVariantWaveQ = 13;     // unified walk scheduled per wave over per-XCD queues
-                                           // (default for spp >= 8), 7 waves/SIMD
-constexpr uint32_t kVariantWaveQLds = 14;  // 13 + wave-uniform leaves fetched once into LDS
-constexpr uint32_t kLeafBuf = 16;          // spheres per wave in the LDS leaf buffer
-constexpr uint32_t kVariantWaveQSmem = 15; // 13 + wave-uniform leaves read by scalar loads
-constexpr uint32_t kVariantWaveQLane = 12; // 13 + one-lane leaf loads, readfirstlane broadcast
-constexpr uint32_t kVariantWaveQ6 = 8;     // 13 at 6 waves/SIMD, no spills (A/B)
-constexpr uint32_t kVariantWaveQ8 = 9;     // 13 compiled for 8 waves/SIMD (A/B)
-constexpr uint32_t kVariantWaveQBundle = 11;  // 13 + bundle-prefiltered leaves (A/B)
-constexpr uint32_t kPrimPad = 4;           // prim_sp padding: scalar reads may run 3 past a leaf
+                                           // (default for spp >= 8)
+// prim_sp padding after the last leaf list: the leaf loads run kChunk - 1 = 1
+// sphere past a leaf's end (rt_capi.cpp fills it)
+constexpr uint32_t kPrimPad = 4;
 
 // A/B toggles (rt_config.flags bits 20..27), results identical either way
 constexpr uint32_t kOptDeviceBuildRefuse = 1u << 0;  // bit 0: treat every tree as too large for
@@ -38,7 +32,10 @@ constexpr uint32_t kOptBtsShift = 1;       // bits 1..3: force the block-tile si
                                            // 0 auto, 1 = 16, 2 = 8, 3 = 4, 4 = 2 pixels
 constexpr uint32_t kOptNoWgCap = 1u << 7; // bit 7: 1-spp frames without the 3-workgroups-per-CU cap
 constexpr uint32_t kOptChunkShift = 4;     // bits 4..6: wave-queue tiles per ticket: 0 auto
-                                           // (4 / rounds, at least 1), k = 1..4 -> 1 << (k - 1)
+                                           // (4 / rounds, at least 1), k = 1..4 -> 1 << (k - 1);
+                                           // 5..7 are refused (a ticket must not span half
+                                           // a slot: the two-level queue's claim rule)
+constexpr uint32_t kOptChunkMax = 4;
 
 // Depth-K cell table (cell_table.hip): entry = {record.x, record.y (24 bits) |
 // depth << 24 | kind << 29} of the node covering each depth-K cell.
@@ -196,7 +193,6 @@ struct FrameArgs {
     uint32_t tiles_x;   // ceil(W / tile_size)
     unsigned long long* counters;  // [primary, shadow, nodes, prims]
     uint32_t variant;   // scene kernel variant (kVariant*)
-    uint32_t stack_entries;  // packet kernel: LDS stack entries per wave
     // wave mapping (set by launch_scene): a wave = ppw pixels (tw x th) x spw samples
     uint32_t spw, g, ppw, tw, th, rounds;  // g = pow2ceil(spw) lanes per pixel
     uint32_t count_work;  // 1: also count node visits / sphere tests (stats frames)

@@ -107,7 +107,7 @@ class KernelRenderer:
                  light_dir: Sequence[float] = (1.0, 1.0, -1.0), ambient: float = 0.1,
                  variant: int = 0, opt_off: int = 0, host_build: bool = False,
                  progressive: bool = False, cell_table: Optional[int] = None,
-                 compat_fma: bool = False):
+                 compat_fma: bool = False, pad_fill: int = 0):
         lib = _lib.load()
         cfg = RtConfig()
         lib.rt_config_default(ctypes.byref(cfg))
@@ -131,6 +131,10 @@ class KernelRenderer:
             flags |= RT_FLAG_PROGRESSIVE
         if compat_fma:
             flags |= _lib.RT_FLAG_COMPAT_FMA
+        # pad_fill (test-only): 0 zeros, 1 NaN, 2 covering spheres after the last leaf list
+        if not 0 <= int(pad_fill) <= 2:
+            raise ValueError("pad_fill must be 0, 1 or 2")
+        flags |= int(pad_fill) << _lib.RT_FLAG_PAD_FILL_SHIFT
         flags |= (int(variant) & 0xF) << _lib.RT_FLAG_VARIANT_SHIFT
         flags |= (int(opt_off) & 0xFF) << _lib.RT_FLAG_OPT_SHIFT
         # cell_table: None = depth chosen from the tree, 0 = no table, k = depth k

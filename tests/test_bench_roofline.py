@@ -14,9 +14,10 @@ PMC = os.path.join(ROOT, "profiles", "pmc_latest.json")
 SIMDS = 1024  # 256 CUs x 4 SIMDs
 
 
-def _pmc():
+def _pmc(cfg="c3"):
+    """One config's entry of the committed summary ({config name: entry})."""
     with open(PMC) as f:
-        return json.load(f)
+        return json.load(f)[cfg]
 
 
 def test_valu_issue_is_the_bound_when_hbm_traffic_is_tiny():
@@ -62,6 +63,17 @@ def test_stale_pmc_summary_is_refused(tmp_path):
     ent, why = bench.load_pmc(str(p), pmc["config"], 1, kernel_source_id())
     assert ent is not None and why == "ok"
     assert bench.load_pmc(str(p), "c5", 1, kernel_source_id())[0] is None
+
+
+def test_summary_holds_c3_and_c5_with_lane_counters():
+    """the lane-utilisation counters on HEAD's kernel, for C3 and C5."""
+    for cfg in ("c3", "c5"):
+        ent, why = bench.load_pmc(PMC, cfg, 1, kernel_source_id())
+        assert ent is not None, why
+        sq = ent["sq"]
+        assert ent["valu_lane_util"] == pytest.approx(
+            sq["SQ_THREAD_CYCLES_VALU"] / sq["SQ_ACTIVE_INST_VALU"] / 64.0)
+        assert 0.0 < ent["valu_lane_util"] <= 1.0
 
 
 def test_scalar_issue_roof_when_counted():

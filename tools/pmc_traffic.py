@@ -95,6 +95,15 @@ def main():
             res["effective_clock_ghz"] = gui / 8.0 / _median(durs)
         if waves:
             res["valu_insts_per_wave"] = sq.get("SQ_INSTS_VALU", (0, 0))[0] / waves
+        thr = sq.get("SQ_THREAD_CYCLES_VALU", (0, 0))[0]
+        if thr and act:
+            # active lanes per VALU instruction cycle (VERDICT r02's lane
+            # utilisation: SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU of 64)
+            res["valu_lanes_active"] = thr / act
+            res["valu_lane_util"] = thr / act / 64.0
+        wait = sq.get("SQ_WAIT_ANY", (0, 0))[0]
+        if wait and cyc:
+            res["wait_any_frac_of_wave_cycles"] = wait / cyc
         if gui and sq.get("SQ_INSTS_SALU"):
             # per CU-cycle (256 CUs, GRBM_GUI_ACTIVE summed over 8 XCDs)
             sc = sq["SQ_INSTS_SALU"][0] + sq.get("SQ_INSTS_BRANCH", (0, 0))[0]
