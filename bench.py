@@ -258,7 +258,7 @@ def main():
 
     import raytracingstudy_amd as rt
     from raytracingstudy_amd.camera import scene_pose
-    from raytracingstudy_amd.dist import TileSharder
+    from raytracingstudy_amd.dist import TileFramePipeline, TileSharder
 
     if args.same_device:
         if args.backend != "gloo":
@@ -328,33 +328,43 @@ def main():
         packed = slabs[0]
 
     events = []
+    recording = [False]
 
-    def step(i: int, record: bool):
-        k = i % F
-        rk, sk, fk = rs[k], streams[k], frames[k]
-        skp = sk.cuda_stream
-        with torch.cuda.stream(sk):  # the collective below waits for sk's render
-            if record:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record(sk)
-            if not tiled:
-                rk.render(fk.data_ptr(), skp)
-            else:
-                rk.render_tiles(my_ids, ts, slabs[k].data_ptr(), skp)
-            if record:
-                e1.record(sk)
-                events.append((e0, e1))
-            if tiled and not args.shard:
-                # RCCL gather of the equal-size slabs to rank 0, on RCCL's stream
-                gathered, work = sharder.gather(slabs[k], slot=k, async_op=True)
-                if work is not None:
-                    # sk waits for the gather: rank 0 unpacks after it, every
-                    # rank renders slot k's next frame into its slab after it
-                    work.wait()
-                # one unpack launch over all ranks' slabs (padding slots skipped)
-                sharder.unpack_fused(gathered, lambda buf, ids: rk.unpack_tiles(
-                    buf.data_ptr(), ids, ts, fk.data_ptr(), skp))
+    def on_render(k, phase):
+        if not recording[0]:
+            return
+        if phase == 0:
+            events.append([torch.cuda.Event(enable_timing=True), None])
+            events[-1][0].record(streams[k])
+        else:
+            events[-1][1] = torch.cuda.Event(enable_timing=True)
+            events[-1][1].record(streams[k])
+
+    if not tiled:
+        def step(i: int, record: bool):
+            k = i % F
+            recording[0] = record
+            with torch.cuda.stream(streams[k]):
+                on_render(k, 0)
+                rs[k].render(frames[k].data_ptr(), streams[k].cuda_stream)
+                on_render(k, 1)
+    else:
+        # render -> async gather -> work.wait() -> fused unpack, F frames in
+        # flight: raytracingstudy_amd.dist.TileFramePipeline, the same step
+        # tests/test_tiles_dist.py drives with gloo on CPU
+        pipe = TileFramePipeline(
+            sharder, slabs,
+            render=lambda k, slab: rs[k].render_tiles(my_ids, ts, slab.data_ptr(),
+                                                      streams[k].cuda_stream),
+            unpack=lambda k, buf, ids: rs[k].unpack_tiles(buf.data_ptr(), ids, ts,
+                                                          frames[k].data_ptr(),
+                                                          streams[k].cuda_stream),
+            stream=lambda k: torch.cuda.stream(streams[k]),  # the collective waits for it
+            gather=not args.shard, on_render=on_render)
+
+        def step(i: int, record: bool):
+            recording[0] = record
+            pipe.step(i)
 
     # counted rays of one frame on this rank (deterministic; equal to the oracle's)
     if not tiled:

@@ -257,6 +257,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
     auto test = [&](const float4& sp, uint32_t ref) -> bool {
         if (kStats) n_prims += 1;
         RT_BS(kBsTest);
+        if (kAnyHit) RT_BS(kBsTestShadow);
         float th;
         if (isect(o0, o1, o2, d0, d1, d2, sp, tmin, tmax, th, bs)) {
             RT_BS(kBsAccept);
@@ -359,6 +360,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         bool any_hit = false;
         for (uint32_t it = 0, cap = 8u * G + 64u;; ++it) {
             RT_BS(kBsIter);
+            if (kAnyHit) RT_BS(kBsIterShadow);
             uint2 rec = make_uint2(0u, 0u);
             bool have = false;   // rec is a leaf record (else the cell is empty)
             bool inner = false;  // stepped into an internal node: descend next trip
@@ -586,6 +588,7 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
         bool hit = false;
         if (active) {
             RT_BS(kBsPhase);
+            if (phase) RT_BS(kBsPhaseShadow);
             hit = walk<false, kChunk, true, kStats>(S, r0, r1, r2, d0, d1, d2, 0.0f, INFINITY, t,
                                                     idx, n_nodes, n_prims,
                                                     static_cast<uint2*>(stk), any, bs);

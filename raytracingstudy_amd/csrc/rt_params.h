@@ -82,6 +82,9 @@ enum BlockStat : uint32_t {
     kBsPop,           // pops reading the LDS stack (m > 1)
     kBsWalk,          // walks started (root box entered)
     kBsPhase,         // sample phases (primary / shadow) run by the wave
+    kBsIterShadow,    // walk loop trips of shadow (any-hit) walks
+    kBsTestShadow,    // sphere tests of shadow walks
+    kBsPhaseShadow,   // shadow phases run by the wave
     kBlockStats
 };
 

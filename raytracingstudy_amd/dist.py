@@ -18,7 +18,7 @@ import numpy as np
 
 from . import tiles as T
 
-__all__ = ["TileSharder"]
+__all__ = ["TileSharder", "TileFramePipeline"]
 
 
 class TileSharder:
@@ -103,3 +103,64 @@ class TileSharder:
             packed = np.asarray(gathered[k].cpu().numpy()).reshape(-1, self.ts, self.ts, self.channels)
             T.unpack_host(packed[:len(ids)], ids, self.width, self.height, self.ts, out)
         return out
+
+
+class TileFramePipeline:
+    """One step of the multi-GPU tile path, with F frames in flight: exactly
+    what bench.py times on every rank, and what tests/test_tiles_dist.py
+    drives with gloo on CPU.
+
+    Frame i uses slot k = i mod F (its own renderer, stream, slab, receive
+    buffer and frame).  step(i):
+      1. ``render(k, slab_k)``: this rank's tiles into slot k's packed slab;
+      2. ``sharder.gather(slab_k, slot=k, async_op=True)``: the equal-size
+         slabs to rank 0 (on the nccl backend RCCL's stream waits for the
+         render on slot k's stream);
+      3. ``work.wait()``: slot k's stream waits for the gather, so rank 0's
+         unpack and every rank's next render into slab k come after it;
+      4. rank 0: ONE ``unpack(k, buffer, ids)`` over all ranks' slabs
+         (``TileSharder.unpack_fused``, padding slots skipped).
+    ``stream(k)`` returns a context manager that makes slot k's stream
+    current (``torch.cuda.stream``), or None on CPU.  ``gather=False``
+    renders only (a local projection of one rank's share, no collective).
+    ``on_render(k, phase)`` is called with phase 0 / 1 right before / after
+    the render call (bench.py records its HIP events there).
+    """
+
+    def __init__(self, sharder: TileSharder, slabs, render: Callable, unpack: Callable,
+                 stream: Optional[Callable] = None, gather: bool = True,
+                 on_render: Optional[Callable] = None, group=None):
+        self.sharder = sharder
+        self.slabs = list(slabs)
+        self.frames_in_flight = len(self.slabs)
+        self.render = render
+        self.unpack = unpack
+        self.stream = stream
+        self.do_gather = gather
+        self.on_render = on_render
+        self.group = group
+        self.last_work = None  # the collective's Work of the last step (tests)
+
+    def step(self, i: int) -> None:
+        k = i % self.frames_in_flight
+        ctx = self.stream(k) if self.stream is not None else None
+        if ctx is not None:
+            with ctx:
+                self._step(k)
+        else:
+            self._step(k)
+
+    def _step(self, k: int) -> None:
+        slab = self.slabs[k]
+        if self.on_render is not None:
+            self.on_render(k, 0)
+        self.render(k, slab)
+        if self.on_render is not None:
+            self.on_render(k, 1)
+        if not self.do_gather:
+            return
+        gathered, work = self.sharder.gather(slab, group=self.group, slot=k, async_op=True)
+        self.last_work = work
+        if work is not None:
+            work.wait()
+        self.sharder.unpack_fused(gathered, lambda buf, ids: self.unpack(k, buf, ids))

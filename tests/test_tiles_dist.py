@@ -89,17 +89,34 @@ def _rank_main(rank, world, port, w, h, spp, q):
         sh.unpack_fused(gathered, lambda buf, ids: fused.setdefault(
             "img", T.unpack_host(buf.numpy().reshape(-1, 64, 64, 4), ids, w, h)))
         assert np.array_equal(fused["img"], per_rank)
-    # a second frame in flight (bench --inflight): its own receive buffer,
-    # the async form, the same frame
-    g1, work = sh.gather(slab, slot=1, async_op=True)
-    if work is not None:
-        work.wait()
+    # bench.py's timed step itself (dist.TileFramePipeline): 2 frames in
+    # flight, each slot its own slab, receive buffer and frame; the gather is
+    # asynchronous (gloo runs host tensors async: a real Work object), then
+    # work.wait(), then one fused unpack on rank 0
+    from raytracingstudy_amd.dist import TileFramePipeline
+    slabs = [slab, sh.new_slab(torch)]
+    frames = [np.zeros((h, w, 4), np.uint8) for _ in slabs]
+    rendered = []
+
+    def render(k, sl):
+        sl.copy_(slab)  # this rank's tiles (the oracle's, above)
+        rendered.append(k)
+
+    def unpack(k, buf, ids):
+        T.unpack_host(buf.numpy().reshape(-1, 64, 64, 4), ids, w, h, out=frames[k])
+
+    pipe = TileFramePipeline(sh, slabs, render, unpack)
+    works = []
+    for i in range(3):
+        pipe.step(i)
+        works.append(pipe.last_work)
+    assert rendered == [0, 1, 0]
+    assert all(wk is not None and hasattr(wk, "wait") for wk in works)
     if rank == 0:
-        assert g1[0].data_ptr() != gathered[0].data_ptr()
-        fused1 = {}
-        sh.unpack_fused(g1, lambda buf, ids: fused1.setdefault(
-            "img", T.unpack_host(buf.numpy().reshape(-1, 64, 64, 4), ids, w, h)))
-        assert np.array_equal(fused1["img"], per_rank)
+        recv = sh.__dict__["_recv_bufs"]
+        assert recv[0][1].data_ptr() != recv[1][1].data_ptr()  # one receive buffer per slot
+        for f in frames:
+            assert np.array_equal(f, per_rank)
         q.put(per_rank)
     dist.barrier()
     dist.destroy_process_group()

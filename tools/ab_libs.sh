@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# A/B of several builds (build_ab/librt_<name>.so from tools/build_rev.sh, or
+# A/B of several builds (abl/librt_<name>.so from tools/build_rev.sh, or
 # copies of the in-tree library), interleaved per repetition so drift hits all
 # of them alike.  Run on the GPU box from the repo root (build_ab must not be
 # in .gpurunignore for that call).
@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 mkdir -p "$(dirname "$LOG")"
 for i in $(seq "$REPS"); do
   for L in "$@"; do
-    RT_AMD_LIB=build_ab/librt_$L.so timeout -k 10 200 python tools/variants.py --configs "$CFGS" \
+    RT_AMD_LIB=abl/librt_$L.so timeout -k 10 200 python tools/variants.py --configs "$CFGS" \
         --variants 0 --rounds 5 | sed "s/^/$L /" >> "$LOG"
   done
 done

@@ -2,7 +2,7 @@
 """Wave-execution counts of the walk's blocks (diagnostic build).
 
     bash tools/build_flags.sh bstats -DRT_BLOCK_STATS
-    RT_AMD_LIB=build_ab/librt_bstats.so python tools/block_stats.py --configs c3,c5
+    RT_AMD_LIB=abl/librt_bstats.so python tools/block_stats.py --configs c3,c5
 
 One stats frame per config; the library appends, per frame, how many times a
 wave executed each block of walk<> and the active lanes summed over those
@@ -21,7 +21,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 NAMES = ["iter", "jump", "jump_descend", "descend", "internal", "leaf", "leaf_chunk", "test",
-         "sqrt", "accept", "exit", "pop", "walk", "phase"]
+         "sqrt", "accept", "exit", "pop", "walk", "phase", "iter_shadow", "test_shadow",
+         "phase_shadow"]
 
 
 def main():

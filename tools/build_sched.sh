@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Build the library with another machine-scheduler setting into build_ab/librt_<name>.so
+# Build the library with another machine-scheduler setting into abl/librt_<name>.so
 # usage: bash tools/build_sched.sh <name> "<SCHED flags>"   (e.g. "" for the compiler default)
 set -e
 NAME=${1:?name}; SCHEDF=${2-}
@@ -10,7 +10,7 @@ cp -r "$ROOT/raytracingstudy_amd/csrc" "$WT/raytracingstudy_amd/"
 cp "$ROOT"/include/*.h "$ROOT"/include/*.hpp "$WT/include/"
 rm -f "$WT"/raytracingstudy_amd/csrc/*.o
 make -s -C "$WT/raytracingstudy_amd/csrc" ../librt_amd.so SCHED="$SCHEDF" 2>&1 | grep -v hip-link || true
-mkdir -p "$ROOT/build_ab"
-cp "$WT/raytracingstudy_amd/librt_amd.so" "$ROOT/build_ab/librt_$NAME.so"
+mkdir -p "$ROOT/abl"
+cp "$WT/raytracingstudy_amd/librt_amd.so" "$ROOT/abl/librt_$NAME.so"
 rm -rf "$WT"
-echo "built build_ab/librt_$NAME.so with SCHED=[$SCHEDF]"
+echo "built abl/librt_$NAME.so with SCHED=[$SCHEDF]"

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Does a longest-first tile order shorten an N-way share?  (diagnostic)
 
-    RT_AMD_LIB=build_ab/librt_timeline.so python tools/tile_order.py --n 8 --save order.json
+    RT_AMD_LIB=abl/librt_timeline.so python tools/tile_order.py --n 8 --save order.json
     python tools/tile_order.py --n 8 --load order.json
 
 With the timeline build: renders rank 0's share, sums the measured unit
