@@ -327,6 +327,7 @@ int build_scene(rt_renderer* r) {
     sc.spheres = r->d_spheres.p;
     sc.albedo = r->d_albedo.p;
     sc.max_depth = depth;
+    sc.stack_depth = std::max(1u, std::min(depth, in.depth_reached));
     sc.G = static_cast<float>(1u << depth);
     for (int i = 0; i < 3; ++i) {
         sc.rmin[i] = rmin[i];

@@ -194,9 +194,12 @@ __device__ __forceinline__ float isect_h(float o0, float o1, float o2, float d0,
 
 // Ancestor-stack levels per thread: depths 1..D-1, or K..D-1 with a cell table
 // (a pop above depth K jumps through the table instead).
+// Internal nodes sit at depths < stack_depth (the deepest leaf), so pushes
+// never pass index stack_depth - 2 - sb (C5: its tree stops at depth 8 under
+// a depth-12 grid: 2 levels, not 6).
 __host__ __device__ inline uint32_t stack_levels(const SceneArgs& S) {
     const uint32_t sb = S.tab_k ? S.tab_k - 1u : 0u;
-    return S.max_depth > 1u + sb ? S.max_depth - 1u - sb : 1u;
+    return S.stack_depth > 1u + sb ? S.stack_depth - 1u - sb : 1u;
 }
 
 // Grid-space octree walk (DESIGN.md "Octree walk"): mirrored origin so every

@@ -168,6 +168,7 @@ struct SceneArgs {
     uint32_t opt;            // kOpt* toggles (A/B only; 0 = all optimisations on)
     const uint2* tab;        // depth-tab_k cell table, or null (cell_table.hip)
     uint32_t tab_k;          // 0: no table
+    uint32_t stack_depth;    // deepest leaf (sizes the per-lane ancestor stack)
 };
 
 struct FrameArgs {

@@ -69,3 +69,4 @@ def test_variants_independent_of_pad(gpu, oracle, case):
             if rep:
                 bad[f"v{v}_f{fill}"] = rep
     assert not bad, bad
+
