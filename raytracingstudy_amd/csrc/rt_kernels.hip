@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -712,6 +713,136 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
     }
 }
 
+// ---------------------------------------------------------------------------
+// Quadrant-sorted rounds (DESIGN.md 5.1 "Sorted rounds")
+//
+// At spp > 64 a pixel's samples run in rounds of 64, and a round costs its
+// slowest lane.  Where a pixel is about one sphere wide (C5: pixel 0.0017,
+// sphere diameter ~0.003 world units) its samples hit different spheres and
+// their walks diverge; the oracle's walks put the slowest lane at 1.6x the
+// mean (tools/shadow_sim.py).  Samples whose jitter falls in the same pixel
+// quadrant are closer, so this path traces a pixel's samples grouped by
+// quadrant (stable: a quadrant's samples in index order), 64 at a time,
+// parks each colour in the wave's LDS under its sample index, and then sums
+// the rounds exactly as shade_wave_tile does: round r = samples 64r..64r+63,
+// pairwise, rounds in order.  Same colours, same sums, same image; the model
+// predicts 11% fewer primary and 13% fewer shadow trips on C5.
+// ---------------------------------------------------------------------------
+
+constexpr uint32_t kSortMaxRounds = 4;  // up to 256 samples per pixel
+// per wave: colours [3][256] f32, tracing order [256] u8
+constexpr uint32_t kSortWaveBytes = 3u * 64u * kSortMaxRounds * 4u + 64u * kSortMaxRounds;
+static_assert(kSortWaveBytes % 16u == 0u, "per-wave regions stay float4-aligned");
+
+// rank of this lane among the lanes set in m
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+}
+
+// jitter quadrant of sample sg (bit 31 of each hash = its u01 >= 0.5)
+__device__ __forceinline__ uint32_t jitter_quadrant(uint32_t hp, uint32_t sg) {
+    return (mix32(hp ^ (sg << 1)) >> 31) | ((mix32(hp ^ ((sg << 1) | 1u)) >> 31) << 1);
+}
+
+// One pixel (spw = 64: the wave is one pixel, lane = sample within a round),
+// 2..4 rounds, at pixel (x, y).
+template <bool kTiles, int kChunk, bool kStats, bool kProg>
+__device__ __forceinline__ void shade_pixel_sorted(const FrameArgs& a, float* wl, void* stk,
+                                                   uint32_t x, uint32_t y, uint32_t obase,
+                                                   uint32_t& n_primary, uint32_t& n_shadow,
+                                                   uint32_t& n_nodes, uint32_t& n_prims,
+                                                   uint32_t* bs) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t R = a.rounds;
+    const bool lane_pix = x < a.W && y < a.H;
+    const uint32_t n = lane_pix ? a.spp : 0u;  // this pixel's samples (local indices)
+    const uint32_t hp = mix32(a.seedmix ^ (y * a.W + x));
+    const uint32_t s_base = kProg ? a.s_base : 0u;
+    float* cr = wl;
+    float* cg = wl + 64u * kSortMaxRounds;
+    float* cb = wl + 2u * 64u * kSortMaxRounds;
+    uint8_t* ord = reinterpret_cast<uint8_t*>(wl + 3u * 64u * kSortMaxRounds);
+    // 1. tracing order: local samples s = 64 j + lane grouped by quadrant
+    //    (4 = no sample), counted by ballots, placed by rank
+    const bool jit = kernargs()->jitter != 0u;
+    auto quad = [&](uint32_t j) -> uint32_t {  // recomputed, not kept live (registers)
+        const uint32_t sl = 64u * j + lane;
+        return sl < n ? (jit ? jitter_quadrant(hp, s_base + sl) : 0u) : 4u;
+    };
+    uint32_t cnt[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t j = 0; j < R; ++j) {
+        const uint32_t qj = quad(j);
+#pragma unroll
+        for (uint32_t q = 0; q < 4u; ++q) cnt[q] += static_cast<uint32_t>(__popcll(__ballot(qj == q)));
+    }
+    uint32_t run[4] = {0u, cnt[0], cnt[0] + cnt[1], cnt[0] + cnt[1] + cnt[2]};
+    for (uint32_t j = 0; j < R; ++j) {
+        const uint32_t qj = quad(j);
+#pragma unroll
+        for (uint32_t q = 0; q < 4u; ++q) {
+            const uint64_t m = __ballot(qj == q);
+            if (qj == q) ord[run[q] + lane_rank(m)] = static_cast<uint8_t>(64u * j + lane);
+            run[q] += static_cast<uint32_t>(__popcll(m));
+        }
+    }
+    // (a wave's LDS operations complete in order: no barrier needed)
+    // 2. trace in that order, each colour parked under its sample index
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t i = 64u * r + lane;
+        const bool valid = i < n;
+        const uint32_t sl = valid ? static_cast<uint32_t>(ord[i]) : 0u;
+        n_primary += static_cast<uint32_t>(__popcll(__ballot(valid)));  // wave-uniform
+        const PixelOut c = sample_color_unified<kChunk, kStats>(a, x, y, hp, s_base + sl, valid,
+                                                                n_shadow, n_nodes, n_prims, stk, bs);
+        if (valid) {
+            cr[sl] = c.r;
+            cg[sl] = c.g;
+            cb[sl] = c.b;
+        }
+    }
+    // 3. the rounds in sample order: pairwise sums (oracle.c:tree_sum), added
+    //    in order (shade_wave_tile's arithmetic)
+    KernArgs* ko = kernargs();
+    float4 A = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t i = 64u * r + lane;
+        PixelOut c{0.0f, 0.0f, 0.0f};
+        if (i < n) c = PixelOut{cr[i], cg[i], cb[i]};
+        for (uint32_t m = 1; m < 64u; m <<= 1) {
+            c.r += __shfl_xor(c.r, static_cast<int>(m), 64);
+            c.g += __shfl_xor(c.g, static_cast<int>(m), 64);
+            c.b += __shfl_xor(c.b, static_cast<int>(m), 64);
+        }
+        if (r == 0u) {
+            if (kProg && ko->accum_in && lane_pix) {
+                const float4 P = ko->accum[(size_t)y * ko->W + x];
+                A = make_float4(P.x + c.r, P.y + c.g, P.z + c.b, 0.0f);
+            } else {
+                A = make_float4(c.r, c.g, c.b, 0.0f);
+            }
+        } else {
+            A = make_float4(A.x + c.r, A.y + c.g, A.z + c.b, 0.0f);
+        }
+    }
+    if (lane == 0u) {
+        if (lane_pix) {
+            if (kProg) ko->accum[(size_t)y * ko->W + x] = A;
+            const float isp = ko->inv_spp;
+            const PixelOut p{A.x * isp, A.y * isp, A.z * isp};
+            const uint32_t rgba = pack_rgba8(p);
+            if (kTiles) {
+                ko->out8[obase + y * ko->tile_size + x] = rgba;
+            } else {
+                ko->out8[(size_t)y * ko->W + x] = rgba;
+                if (ko->out32) ko->out32[(size_t)y * ko->W + x] = make_float4(p.r, p.g, p.b, 1.0f);
+            }
+        } else if (kTiles) {
+            ko->out8[obase + y * ko->tile_size + x] = 0u;  // off-image pixel of an edge tile
+        }
+    }
+}
+
 // Work scheduling (persistent workgroups: grid = resident workgroups):
 //
 // kWaveQ = false: workgroups pull bts x bts block tiles from ONE device-wide
@@ -735,12 +866,19 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
 // waves fit: C3 -1.9%, its tile path -3.3%, C5 -2.4% (84: 8 do not fit; 76
 // and 72: the extra spills cost more; profiles/r02/sgpr_ab.log).
 // scene_kernel_w8 below is that build of the timed default.
-template <bool kTiles, int kChunk, bool kStats = true, bool kProg = false, bool kWaveQ = false>
+template <bool kTiles, int kChunk, bool kStats = true, bool kProg = false, bool kWaveQ = false,
+          bool kSort = false>
 __device__ __forceinline__ void scene_body(FrameArgs a) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     float4* acc = lds;  // [256] running pixel sums (leader lanes' slots)
     const uint32_t wave = threadIdx.x >> 6;
-    void* stk = reinterpret_cast<uint2*>(lds + kBlockThreads) + threadIdx.x;
+    // sorted rounds: no per-thread pixel sums; stacks first, then each wave's
+    // colours and tracing order (sort_lds_bytes)
+    void* stk = reinterpret_cast<uint2*>(lds + (kSort ? 0u : kBlockThreads)) + threadIdx.x;
+    float* wl = kSort ? reinterpret_cast<float*>(reinterpret_cast<uint2*>(lds) +
+                                                 stack_levels(a.sc) * kBlockThreads) +
+                            wave * (kSortWaveBytes / 4u)
+                      : nullptr;
     const uint32_t tw = a.tw, th = a.th;
     uint32_t n_shadow = 0, n_nodes = 0, n_prims = 0, n_primary = 0;
 #ifdef RT_BLOCK_STATS
@@ -865,8 +1003,12 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
 #ifdef RT_TIMELINE
                 const unsigned long long tu0 = wall_clock64();
 #endif
-                shade_wave_tile<kTiles, kChunk, kStats, kProg>(
-                    a, acc, stk, ox, oy, obase, n_primary, n_shadow, n_nodes, n_prims, bs);
+                if (kSort)
+                    shade_pixel_sorted<kTiles, kChunk, kStats, kProg>(
+                        a, wl, stk, ox, oy, obase, n_primary, n_shadow, n_nodes, n_prims, bs);
+                else
+                    shade_wave_tile<kTiles, kChunk, kStats, kProg>(
+                        a, acc, stk, ox, oy, obase, n_primary, n_shadow, n_nodes, n_prims, bs);
 #ifdef RT_TIMELINE
                 // per unit {start, end, hw_id << 32 | xcc << 16 | wave index}
                 // after the 65536 per-wave records
@@ -944,17 +1086,17 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
 }
 
 template <bool kTiles, int kMinW, int kChunk, bool kStats = true, bool kProg = false,
-          bool kWaveQ = false>
+          bool kWaveQ = false, bool kSort = false>
 __global__ void __launch_bounds__(kBlockThreads, kMinW) scene_kernel(FrameArgs a) {
-    scene_body<kTiles, kChunk, kStats, kProg, kWaveQ>(a);
+    scene_body<kTiles, kChunk, kStats, kProg, kWaveQ, kSort>(a);
 }
 
 // The timed default for spp >= 8 (variant 13, plain frames): 8 waves per SIMD,
 // SGPRs capped so that they fit (see above).
-template <bool kTiles, bool kProg = false>
+template <bool kTiles, bool kProg = false, bool kSort = false>
 __global__ void __launch_bounds__(kBlockThreads, 8) __attribute__((amdgpu_num_sgpr(80)))
     scene_kernel_w8(FrameArgs a) {
-    scene_body<kTiles, 2, false, kProg, true>(a);
+    scene_body<kTiles, 2, false, kProg, true, kSort>(a);
 }
 
 __global__ void __launch_bounds__(kBlockThreads)
@@ -1110,8 +1252,40 @@ static void launch_waveq(K kernel, const FrameArgs& a, size_t lds, hipStream_t s
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlockThreads), lds, st, b);
 }
 
+// Sorted rounds (above): a wave-queue frame of one pixel per wave and 2..4
+// rounds, wherever the per-wave LDS still lets 8 workgroups share a CU.
+// RT_SORT=0 turns it off (A/B; images and counters are the same).
+static uint32_t env_u32(const char* name, uint32_t dflt) {
+    const char* e = getenv(name);
+    return e && *e ? static_cast<uint32_t>(strtoul(e, nullptr, 10)) : dflt;
+}
+size_t sort_lds_bytes(const FrameArgs& a) {
+    return static_cast<size_t>(stack_levels(a.sc)) * kBlockThreads * sizeof(uint2) +
+           (kBlockThreads / 64) * kSortWaveBytes;
+}
+static bool sorted_rounds(const FrameArgs& a) {
+    static const uint32_t on = env_u32("RT_SORT", 1u);
+    return on && a.spp >= 8u && a.spw == 64u && a.rounds >= 2u && a.rounds <= kSortMaxRounds &&
+           sort_lds_bytes(a) * 8u <= 160u * 1024u &&
+           (a.accum != nullptr || a.variant == kVariantWaveQ);
+}
+
 template <bool kTiles>
 static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStream_t st) {
+    if (sorted_rounds(a)) {
+        const size_t sl = sort_lds_bytes(a);
+        if (a.accum) {
+            if (a.count_work)
+                launch_waveq(scene_kernel<kTiles, 7, 2, true, true, true, true>, a, sl, st);
+            else
+                launch_waveq(scene_kernel_w8<kTiles, true, true>, a, sl, st, 8);
+        } else if (a.count_work) {
+            launch_waveq(scene_kernel<kTiles, 7, 2, true, false, true, true>, a, sl, st);
+        } else {
+            launch_waveq(scene_kernel_w8<kTiles, false, true>, a, sl, st, 8);
+        }
+        return;
+    }
     if (a.accum) {  // progressive frames: the unified walk, whatever the variant
         if (a.spp >= 8u) {  // the wave queue, like variant 13
             if (a.count_work)

@@ -70,3 +70,62 @@ def test_variants_independent_of_pad(gpu, oracle, case):
                 bad[f"v{v}_f{fill}"] = rep
     assert not bad, bad
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,w,h,spp,jitter,tiles", [
+    (30000, 70, 45, 256, None, False),   # four rounds (C5's shape), edge pixels
+    (30000, 70, 45, 192, None, True),    # three rounds, packed tiles with off-image pixels
+    (30000, 33, 20, 100, None, False),   # a partial second round
+    (30000, 33, 20, 128, False, False),  # no jitter: every sample in quadrant 0
+])
+def test_sorted_rounds_match_oracle(gpu, oracle, n, w, h, spp, jitter, tiles):
+    """Quadrant-sorted rounds (spp 65..256): the samples are traced out of
+    order, parked and summed in order; image, radiance and counters stay the
+    oracle's, plain and stats frames alike."""
+    import ctypes
+    sp, al = rt.generate_spheres(n, rt.SEED)
+    pose = rt.camera.scene_pose()
+    with rt.KernelRenderer(w, h, mode="scene", spp=spp, radiance=True, jitter=jitter) as r:
+        r.resize(w, h)
+        r.setPosition(pose)
+        r.set_scene(sp, al)
+        r.render()
+        img0, rad0 = r.readback(), r.readback_radiance()
+        st = r.render(stats=True)
+        img, rad = r.readback(), r.readback_radiance()
+        _, K = r.camera()
+        if tiles:
+            ids = np.arange(((w + 63) // 64) * ((h + 63) // 64), dtype=np.uint32)[::-1].copy()
+            hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
+            buf = ctypes.c_void_p()
+            assert hip.hipMalloc(ctypes.byref(buf), ctypes.c_size_t(len(ids) * 64 * 64 * 4)) == 0
+            try:
+                r.render_tiles(ids, 64, buf.value)
+                r.unpack_tiles(buf.value, ids, 64)
+                assert np.array_equal(r.readback(), img)
+            finally:
+                hip.hipFree(buf)
+    ref = oracle.Scene(sp, al).render(w, h, pose, K, spp=spp, jitter=jitter)
+    rep = vc.diff_report(img, rad, st, ref)
+    assert not rep, rep
+    assert np.array_equal(img0, img) and np.array_equal(rad0, rad)
+
+
+@pytest.mark.gpu
+def test_sorted_rounds_progressive(gpu, oracle):
+    """Progressive frames of 128 spp (two sorted rounds each) accumulate to
+    the oracle's 384-spp image."""
+    n, w, h = 30000, 40, 30
+    sp, al = rt.generate_spheres(n, rt.SEED)
+    pose = rt.camera.scene_pose()
+    with rt.KernelRenderer(w, h, mode="scene", spp=128, progressive=True, radiance=True) as p:
+        p.resize(w, h)
+        p.setPosition(pose)
+        p.set_scene(sp, al)
+        for _ in range(3):
+            p.render()
+        img = p.readback()
+        _, K = p.camera()
+    ref8, _, _ = oracle.Scene(sp, al).render(w, h, pose, K, spp=384)
+    assert np.array_equal(img, ref8)
