@@ -730,8 +730,10 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
 // ---------------------------------------------------------------------------
 
 constexpr uint32_t kSortMaxRounds = 4;  // up to 256 samples per pixel
-// per wave: colours [3][256] f32, tracing order [256] u8
-constexpr uint32_t kSortWaveBytes = 3u * 64u * kSortMaxRounds * 4u + 64u * kSortMaxRounds;
+constexpr uint32_t kSortMax = 64u * kSortMaxRounds;
+// per wave: per sample a slot {t, sphere} -> {lam | miss g, albedo | miss b}
+// and a kind byte; the tracing order and the list of lit samples (u8 each)
+constexpr uint32_t kSortWaveBytes = kSortMax * 8u + 3u * kSortMax;
 static_assert(kSortWaveBytes % 16u == 0u, "per-wave regions stay float4-aligned");
 
 // rank of this lane among the lanes set in m
@@ -745,26 +747,67 @@ __device__ __forceinline__ uint32_t jitter_quadrant(uint32_t hp, uint32_t sg) {
     return (mix32(hp ^ (sg << 1)) >> 31) | ((mix32(hp ^ ((sg << 1) | 1u)) >> 31) << 1);
 }
 
-// One pixel (spw = 64: the wave is one pixel, lane = sample within a round),
-// 2..4 rounds, at pixel (x, y).
+// Primary ray direction of sample sg of pixel (x, y) (sample_color_unified's).
+__device__ __forceinline__ void sample_dir(uint32_t x, uint32_t y, uint32_t hp, uint32_t sg,
+                                           float& d0, float& d1, float& d2) {
+    KernArgs* ka = kernargs();
+    float u = static_cast<float>(x), v = static_cast<float>(y);
+    if (ka->jitter) {
+        u = u + u01(mix32(hp ^ (sg << 1)));
+        v = v + u01(mix32(hp ^ ((sg << 1) | 1u)));
+    }
+    CamArgs cam;
+    for (int i = 0; i < 9; ++i) cam.K[i] = ka->cam.K[i], cam.R[i] = ka->cam.R[i];
+    get_ray(cam, u, v, d0, d1, d2);
+}
+
+// Hit point and normal of a primary hit (sample_color_unified's shading prep).
+struct HitShade {
+    float p0, p1, p2, n0, n1, n2, ndl;
+};
+__device__ __forceinline__ HitShade hit_shade(float d0, float d1, float d2, float t, uint32_t idx) {
+    KernArgs* kb = kernargs();
+    const float4 sp = kb->sc.spheres[idx];
+    HitShade h;
+    h.p0 = kb->cam.o[0] + t * d0;
+    h.p1 = kb->cam.o[1] + t * d1;
+    h.p2 = kb->cam.o[2] + t * d2;
+    const float ir = 1.0f / sp.w;
+    h.n0 = (h.p0 - sp.x) * ir;
+    h.n1 = (h.p1 - sp.y) * ir;
+    h.n2 = (h.p2 - sp.z) * ir;
+    h.ndl = h.n0 * kb->L[0] + h.n1 * kb->L[1] + h.n2 * kb->L[2];
+    return h;
+}
+
+// One pixel (spw = 64: the wave is one pixel), 2..4 rounds, at pixel (x, y):
+//  1. order: the pixel's samples grouped by jitter quadrant;
+//  2. primary rays 64 at a time in that order; a miss or an unlit hit is
+//     final (its slot holds the colour's inputs), a lit hit parks {t, sphere}
+//     and joins the list of lit samples;
+//  3. the lit samples' shadow rays 64 at a time (dense: one pixel's lit
+//     samples of all rounds together, in quadrant order), each recomputing
+//     its hit point from {t, sphere} with the same operations;
+//  4. per round in sample order: colours, pairwise sums, rounds in order.
 template <bool kTiles, int kChunk, bool kStats, bool kProg>
 __device__ __forceinline__ void shade_pixel_sorted(const FrameArgs& a, float* wl, void* stk,
                                                    uint32_t x, uint32_t y, uint32_t obase,
                                                    uint32_t& n_primary, uint32_t& n_shadow,
                                                    uint32_t& n_nodes, uint32_t& n_prims,
                                                    uint32_t* bs) {
+    const SceneArgs& S = a.sc;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t R = a.rounds;
     const bool lane_pix = x < a.W && y < a.H;
     const uint32_t n = lane_pix ? a.spp : 0u;  // this pixel's samples (local indices)
     const uint32_t hp = mix32(a.seedmix ^ (y * a.W + x));
     const uint32_t s_base = kProg ? a.s_base : 0u;
-    float* cr = wl;
-    float* cg = wl + 64u * kSortMaxRounds;
-    float* cb = wl + 2u * 64u * kSortMaxRounds;
-    uint8_t* ord = reinterpret_cast<uint8_t*>(wl + 3u * 64u * kSortMaxRounds);
-    // 1. tracing order: local samples s = 64 j + lane grouped by quadrant
-    //    (4 = no sample), counted by ballots, placed by rank
+    uint2* slot = reinterpret_cast<uint2*>(wl);
+    uint8_t* kind = reinterpret_cast<uint8_t*>(slot + kSortMax);  // 0 miss, 1 hit, 2 lit (in flight)
+    uint8_t* ord = kind + kSortMax;
+    uint8_t* lit = ord + kSortMax;
+    // 1. tracing order: local samples s = 64 j + lane grouped by quadrant (4 =
+    //    no sample), counted by ballots, placed by rank
     const bool jit = kernargs()->jitter != 0u;
     auto quad = [&](uint32_t j) -> uint32_t {  // recomputed, not kept live (registers)
         const uint32_t sl = 64u * j + lane;
@@ -787,28 +830,104 @@ __device__ __forceinline__ void shade_pixel_sorted(const FrameArgs& a, float* wl
         }
     }
     // (a wave's LDS operations complete in order: no barrier needed)
-    // 2. trace in that order, each colour parked under its sample index
+    // 2. primary rays in that order
+    uint32_t nl = 0;  // lit samples listed (wave-uniform)
     for (uint32_t r = 0; r < R; ++r) {
         const uint32_t i = 64u * r + lane;
         const bool valid = i < n;
         const uint32_t sl = valid ? static_cast<uint32_t>(ord[i]) : 0u;
         n_primary += static_cast<uint32_t>(__popcll(__ballot(valid)));  // wave-uniform
-        const PixelOut c = sample_color_unified<kChunk, kStats>(a, x, y, hp, s_base + sl, valid,
-                                                                n_shadow, n_nodes, n_prims, stk, bs);
+        float d0, d1, d2;
+        sample_dir(x, y, hp, s_base + sl, d0, d1, d2);
+        float t = 0.0f;
+        uint32_t idx = 0;
+        bool hit = false;
         if (valid) {
-            cr[sl] = c.r;
-            cg[sl] = c.g;
-            cb[sl] = c.b;
+            RT_BS(kBsPhase);
+            KernArgs* kc = kernargs();
+            hit = walk<false, kChunk, true, kStats>(S, kc->cam.o[0], kc->cam.o[1], kc->cam.o[2], d0,
+                                                    d1, d2, 0.0f, INFINITY, t, idx, n_nodes,
+                                                    n_prims, static_cast<uint2*>(stk), false, bs);
+        }
+        bool is_lit = false;
+        if (valid) {
+            uint2 sv = make_uint2(__float_as_uint(sat(d1)), __float_as_uint(sat(d2)));
+            uint8_t kd = 0;
+            if (hit) {
+                const HitShade h = hit_shade(d0, d1, d2, t, idx);
+                is_lit = h.ndl > 0.0f && kernargs()->shadows;
+                if (is_lit) {
+                    sv = make_uint2(__float_as_uint(t), idx);
+                    kd = 2;
+                } else {
+                    sv = make_uint2(__float_as_uint(h.ndl > 0.0f ? h.ndl : 0.0f),
+                                    kernargs()->sc.albedo[idx]);
+                    kd = 1;
+                }
+            }
+            slot[sl] = sv;
+            kind[sl] = kd;
+        }
+        const uint64_t lm = __ballot(is_lit);
+        if (is_lit) lit[nl + lane_rank(lm)] = static_cast<uint8_t>(sl);
+        nl += static_cast<uint32_t>(__popcll(lm));
+    }
+    n_shadow += nl;
+    // 3. the lit samples' shadow rays, 64 at a time
+    for (uint32_t c0 = 0; c0 < nl; c0 += 64u) {
+        const uint32_t j = c0 + lane;
+        const bool has = j < nl;
+        const uint32_t sl = has ? static_cast<uint32_t>(lit[j]) : 0u;
+        float o0 = 0.f, o1 = 0.f, o2 = 0.f, lam = 0.0f;
+        uint32_t idx = 0;
+        if (has) {
+            float d0, d1, d2;
+            sample_dir(x, y, hp, s_base + sl, d0, d1, d2);
+            const uint2 sv = slot[sl];
+            idx = sv.y;
+            const HitShade h = hit_shade(d0, d1, d2, __uint_as_float(sv.x), idx);
+            lam = h.ndl > 0.0f ? h.ndl : 0.0f;
+            o0 = h.p0 + h.n0 * kShadowEps;
+            o1 = h.p1 + h.n1 * kShadowEps;
+            o2 = h.p2 + h.n2 * kShadowEps;
+        }
+        bool occ = false;
+        if (has) {
+            RT_BS(kBsPhase);
+            RT_BS(kBsPhaseShadow);
+            KernArgs* kl = kernargs();
+            float ts;
+            uint32_t is;
+            occ = walk<false, kChunk, true, kStats>(S, o0, o1, o2, kl->L[0], kl->L[1], kl->L[2], 0.0f,
+                                                    INFINITY, ts, is, n_nodes, n_prims,
+                                                    static_cast<uint2*>(stk), true, bs);
+        }
+        if (has) {
+            slot[sl] = make_uint2(__float_as_uint(occ ? 0.0f : lam), kernargs()->sc.albedo[idx]);
+            kind[sl] = 1;
         }
     }
-    // 3. the rounds in sample order: pairwise sums (oracle.c:tree_sum), added
-    //    in order (shade_wave_tile's arithmetic)
+    // 4. the rounds in sample order: colours, pairwise sums (oracle.c:tree_sum),
+    //    added in order (shade_wave_tile's arithmetic)
     KernArgs* ko = kernargs();
     float4 A = make_float4(0.f, 0.f, 0.f, 0.f);
     for (uint32_t r = 0; r < R; ++r) {
         const uint32_t i = 64u * r + lane;
         PixelOut c{0.0f, 0.0f, 0.0f};
-        if (i < n) c = PixelOut{cr[i], cg[i], cb[i]};
+        if (i < n) {
+            const uint2 sv = slot[i];
+            if (kind[i]) {
+                const float lam = __uint_as_float(sv.x);
+                const uint32_t al = sv.y;
+                const float amb = ko->ambient;
+                const float f = amb + (1.0f - amb) * lam;
+                c.r = static_cast<float>(al & 0xFFu) * (1.0f / 255.0f) * f;
+                c.g = static_cast<float>((al >> 8) & 0xFFu) * (1.0f / 255.0f) * f;
+                c.b = static_cast<float>((al >> 16) & 0xFFu) * (1.0f / 255.0f) * f;
+            } else {
+                c = PixelOut{200.0f / 255.0f, __uint_as_float(sv.x), __uint_as_float(sv.y)};
+            }
+        }
         for (uint32_t m = 1; m < 64u; m <<= 1) {
             c.r += __shfl_xor(c.r, static_cast<int>(m), 64);
             c.g += __shfl_xor(c.g, static_cast<int>(m), 64);
