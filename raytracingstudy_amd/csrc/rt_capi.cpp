@@ -9,6 +9,7 @@
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -225,7 +226,21 @@ int build_scene(rt_renderer* r) {
         if (res.ref_overflow || e == hipErrorOutOfMemory) {
             // the device builder's 32-bit per-level slots (or HBM) cannot hold
             // this tree: build the identical tree on the host instead
+            // (rt_scene_info.builder then reports RT_BUILDER_HOST).  Bound the
+            // attempt first: the host builder holds at least the overflowing
+            // level's references (index + sphere record + per-level lists,
+            // ~64 B each); refuse at once rather than page for minutes
             (void)hipGetLastError();
+            const uint64_t need = res.ref_overflow * 64ull;
+            const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGE_SIZE);
+            const uint64_t phys = pages > 0 && psz > 0 ? uint64_t(pages) * uint64_t(psz) : 0ull;
+            if (phys && need > phys / 2)
+                return fail(r, RT_E_NOMEM,
+                            "scene too large for the octree: the device builder overflowed at " +
+                                std::to_string(res.ref_overflow) +
+                                " references and the host builder would need about " +
+                                std::to_string(need >> 30) + " GiB; lower max_depth or raise "
+                                "leaf_capacity");
             host = true;
         } else if (e != hipSuccess) {
             return hip_fail(r, e, "device octree build");

@@ -195,10 +195,14 @@ __device__ __forceinline__ float isect_h(float o0, float o1, float o2, float d0,
 
 // Ancestor-stack levels per thread: depths 1..D-1, or K..D-1 with a cell table
 // (a pop above depth K jumps through the table instead).
-// Internal nodes sit at depths < stack_depth (the deepest leaf), so pushes
-// never pass index stack_depth - 2 - sb (C5: its tree stops at depth 8 under
-// a depth-12 grid: 2 levels, not 6).
-__host__ __device__ inline uint32_t stack_levels(const SceneArgs& S) {
+// Per-thread ancestor-stack levels.  Internal nodes sit at depths <
+// stack_depth (the deepest leaf), and with a cell table only depths >= K are
+// pushed: K .. stack_depth - 1 (C5: its tree stops at depth 8 under a
+// depth-12 grid, so 2 levels, not 6).  The stackless walk (kNoStack, sorted
+// pixels) keeps none when there is a table: an ancestor that is not the
+// current node re-enters through the table.
+__host__ __device__ inline uint32_t stack_levels(const SceneArgs& S, bool no_stack = false) {
+    if (no_stack && S.tab_k) return 0u;
     const uint32_t sb = S.tab_k ? S.tab_k - 1u : 0u;
     return S.stack_depth > 1u + sb ? S.stack_depth - 1u - sb : 1u;
 }
@@ -211,7 +215,8 @@ __host__ __device__ inline uint32_t stack_levels(const SceneArgs& S) {
 // The per-thread ancestor stack lives in LDS, [depth-1][thread] (conflict-free).
 // kAnyHit: compile-time any-hit; with kDynAny the mode comes from `any_rt`
 // instead, so ONE inlined walk serves both the primary and the shadow ray.
-template <bool kAnyHitT, int kChunk = 2, bool kDynAny = false, bool kStats = true>
+template <bool kAnyHitT, int kChunk = 2, bool kDynAny = false, bool kStats = true,
+          bool kNoStack = false>
 __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, float o2, float d0,
                                      float d1, float d2, float tmin, float tmax, float& tout,
                                      uint32_t& iout, uint32_t& n_nodes, uint32_t& n_prims,
@@ -353,7 +358,8 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         const uint32_t K = S.tab_k;
         bool jump = tab != nullptr;
         uint32_t from = 0;  // depth the oracle re-descends from (stats)
-        // with a table, only depths >= K are ever on the stack (stack_levels)
+        // with a table, only depths >= K are ever on the stack (stack_levels);
+        // the stackless walk (kNoStack) keeps one only without a table
         const uint32_t sb = K ? K - 1u : 0u;
         // Hard cap (never reached by a correct walk: a ray crosses < 3*G cells
         // and each crossing costs at most one descent): no input can hang the GPU.
@@ -397,7 +403,11 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 rec = make_uint2(e.x, e.y & kCellRecMask);
                 // the oracle reads one record per level from `from` down to
                 // the covering node (an empty child's own level reads none)
-                if (kStats) n_nodes += (kind == kCellEmpty ? depth - 1u : depth) - from;
+                // (a re-entry below K re-reads levels the oracle pops: none counted)
+                if (kStats) {
+                    const uint32_t cd = kind == kCellEmpty ? depth - 1u : depth;
+                    n_nodes += cd > from ? cd - from : 0u;
+                }
                 inner = kind == kCellInternal;
                 have = kind == kCellLeaf;
             } else {
@@ -418,7 +428,9 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 if (have) {
                     const uint32_t slot = node.x + __builtin_popcount(valid & ((1u << child) - 1u));
                     rec = nodes[slot];
-                    if (kStats) n_nodes += 1;
+                    // records down to a re-entered ancestor are the oracle's
+                    // stack pops, not reads
+                    if (kStats && depth > from) n_nodes += 1;
                     inner = !((node.y >> 8) & (1u << child));
                     have = !inner;
                 }
@@ -433,7 +445,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             if (inner) {
                 RT_BS(kBsInternal);
                 node = rec;
-                stk[(depth - 1 - sb) * kBlockThreads] = rec;
+                if (!kNoStack || !tab) stk[(depth - 1 - sb) * kBlockThreads] = rec;
             } else {
                 if (have) any_hit = leaf(rec.x, rec.y);
                 RT_BS(kBsExit);
@@ -456,18 +468,21 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 const uint32_t diff = (l0 ^ n0) | (l1 ^ n1) | (l2 ^ n2);
                 const uint32_t top = 31u - __builtin_clz(diff);  // highest flipped bit
                 t = texit;
-                // The common ancestor: size 2^(top+1), depth D - (top+1).  Above the
-                // table level the walk jumps: a cell at depth >= K indexes the table
-                // straight from the neighbour's corner (`keep`), a shallower one
-                // resolves down to K from the ancestor's cell.  Otherwise it pops
-                // to the ancestor.  Selects, not branches: every lane ends the trip
-                // with the same instructions (the scalar pipe carries the branches'
-                // exec-mask updates, and it is the kernel's busiest unit).
+                // The common ancestor: size 2^(top+1), depth D - (top+1).  With a
+                // table the walk re-enters through it unless the ancestor is the
+                // node it iterates (m == 1): above depth K, or (no ancestor stack)
+                // two or more levels up.  A cell at depth >= K indexes the table
+                // straight from the neighbour's corner (`keep`) and re-descends
+                // by records; a shallower one resolves down to K from the
+                // ancestor's cell.  Without a table it pops to the ancestor.
+                // Selects, not branches: every lane ends the trip with the same
+                // instructions (the scalar pipe carries the branches' exec-mask
+                // updates, and it is the kernel's busiest unit).
                 const uint32_t adepth = D - (top + 1u);
-                const bool above = adepth < K;
+                const uint32_t m = depth - adepth;  // levels up to the ancestor
+                const bool above = adepth < K || (kNoStack && K != 0u && m > 1u);
                 const bool keep = above && depth >= K;
                 const uint32_t asize = 2u << top;
-                const uint32_t m = depth - adepth;  // levels popped (when !above)
                 const uint32_t am = keep ? 0xFFFFFFFFu : ~(asize - 1u);
                 l0 = n0 & am;
                 l1 = n1 & am;
@@ -477,7 +492,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 if (kStats && above) from = adepth;
                 jump = above;
                 // m == 1: the ancestor is the node we are iterating (still in `node`)
-                if (!stop && !above && m > 1) {
+                if (!stop && !above && m > 1) {  // (the stackless walk: only without a table)
                     RT_BS(kBsPop);
                     node = depth ? stk[(depth - 1 - sb) * kBlockThreads] : S.root;
                 }
@@ -733,7 +748,9 @@ constexpr uint32_t kSortMaxRounds = 4;  // up to 256 samples per pixel
 constexpr uint32_t kSortMax = 64u * kSortMaxRounds;
 // per wave: per sample a slot {t, sphere} -> {lam | miss g, albedo | miss b}
 // and a kind byte; the tracing order and the list of lit samples (u8 each)
-constexpr uint32_t kSortWaveBytes = kSortMax * 8u + 3u * kSortMax;
+constexpr uint32_t kSortCellBits = 3;  // jitter cells per axis: 2^3 (8 x 8, Morton order)
+constexpr uint32_t kSortCells = 1u << (2u * kSortCellBits);
+constexpr uint32_t kSortWaveBytes = kSortMax * 8u + 3u * kSortMax + kSortCells * 4u;
 static_assert(kSortWaveBytes % 16u == 0u, "per-wave regions stay float4-aligned");
 
 // rank of this lane among the lanes set in m
@@ -742,9 +759,17 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
 }
 
-// jitter quadrant of sample sg (bit 31 of each hash = its u01 >= 0.5)
-__device__ __forceinline__ uint32_t jitter_quadrant(uint32_t hp, uint32_t sg) {
-    return (mix32(hp ^ (sg << 1)) >> 31) | ((mix32(hp ^ ((sg << 1) | 1u)) >> 31) << 1);
+// Morton cell of sample sg's jitter on a 2^kSortCellBits grid per axis (the
+// top bits of each hash are its u01 in those steps): the top two bits are
+// the quadrant, and so on down
+__device__ __forceinline__ uint32_t jitter_cell(uint32_t hp, uint32_t sg) {
+    const uint32_t qu = mix32(hp ^ (sg << 1)) >> (32u - kSortCellBits);
+    const uint32_t qv = mix32(hp ^ ((sg << 1) | 1u)) >> (32u - kSortCellBits);
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < kSortCellBits; ++b)
+        c |= (((qu >> b) & 1u) << (2u * b)) | (((qv >> b) & 1u) << (2u * b + 1u));
+    return c;
 }
 
 // Primary ray direction of sample sg of pixel (x, y) (sample_color_unified's).
@@ -806,27 +831,35 @@ __device__ __forceinline__ void shade_pixel_sorted(const FrameArgs& a, float* wl
     uint8_t* kind = reinterpret_cast<uint8_t*>(slot + kSortMax);  // 0 miss, 1 hit, 2 lit (in flight)
     uint8_t* ord = kind + kSortMax;
     uint8_t* lit = ord + kSortMax;
-    // 1. tracing order: local samples s = 64 j + lane grouped by quadrant (4 =
-    //    no sample), counted by ballots, placed by rank
+    // 1. tracing order: local samples s = 64 j + lane grouped by 4x4 Morton
+    //    cell of their jitter (quadrants first): a counting sort over LDS
+    //    counters (an LDS atomic gives a sample its place in its cell)
+    uint32_t* bcnt = reinterpret_cast<uint32_t*>(lit + kSortMax);
     const bool jit = kernargs()->jitter != 0u;
-    auto quad = [&](uint32_t j) -> uint32_t {  // recomputed, not kept live (registers)
+    if (lane < kSortCells) bcnt[lane] = 0u;
+    // (cell << 8 | place in the cell) parked in the sample's slot until placed
+    for (uint32_t j = 0; j < R; ++j) {
         const uint32_t sl = 64u * j + lane;
-        return sl < n ? (jit ? jitter_quadrant(hp, s_base + sl) : 0u) : 4u;
-    };
-    uint32_t cnt[4] = {0u, 0u, 0u, 0u};
-    for (uint32_t j = 0; j < R; ++j) {
-        const uint32_t qj = quad(j);
-#pragma unroll
-        for (uint32_t q = 0; q < 4u; ++q) cnt[q] += static_cast<uint32_t>(__popcll(__ballot(qj == q)));
+        if (sl < n) {
+            const uint32_t cell = jit ? jitter_cell(hp, s_base + sl) : 0u;
+            slot[sl].x = (cell << 8) | atomicAdd(bcnt + cell, 1u);
+        }
     }
-    uint32_t run[4] = {0u, cnt[0], cnt[0] + cnt[1], cnt[0] + cnt[1] + cnt[2]};
-    for (uint32_t j = 0; j < R; ++j) {
-        const uint32_t qj = quad(j);
+    {  // exclusive prefix of the cells' counts (one per lane)
+        const uint32_t v = lane < kSortCells ? bcnt[lane] : 0u;
+        uint32_t incl = v;
 #pragma unroll
-        for (uint32_t q = 0; q < 4u; ++q) {
-            const uint64_t m = __ballot(qj == q);
-            if (qj == q) ord[run[q] + lane_rank(m)] = static_cast<uint8_t>(64u * j + lane);
-            run[q] += static_cast<uint32_t>(__popcll(m));
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(incl, static_cast<unsigned>(d), 64);
+            if (static_cast<int>(lane) >= d) incl += o;
+        }
+        if (lane < kSortCells) bcnt[lane] = incl - v;
+    }
+    for (uint32_t j = 0; j < R; ++j) {
+        const uint32_t sl = 64u * j + lane;
+        if (sl < n) {
+            const uint32_t kp = slot[sl].x;
+            ord[bcnt[kp >> 8] + (kp & 0xFFu)] = static_cast<uint8_t>(sl);
         }
     }
     // (a wave's LDS operations complete in order: no barrier needed)
@@ -845,9 +878,9 @@ __device__ __forceinline__ void shade_pixel_sorted(const FrameArgs& a, float* wl
         if (valid) {
             RT_BS(kBsPhase);
             KernArgs* kc = kernargs();
-            hit = walk<false, kChunk, true, kStats>(S, kc->cam.o[0], kc->cam.o[1], kc->cam.o[2], d0,
-                                                    d1, d2, 0.0f, INFINITY, t, idx, n_nodes,
-                                                    n_prims, static_cast<uint2*>(stk), false, bs);
+            hit = walk<false, kChunk, true, kStats, true>(S, kc->cam.o[0], kc->cam.o[1], kc->cam.o[2],
+                                                          d0, d1, d2, 0.0f, INFINITY, t, idx, n_nodes,
+                                                          n_prims, static_cast<uint2*>(stk), false, bs);
         }
         bool is_lit = false;
         if (valid) {
@@ -898,9 +931,9 @@ __device__ __forceinline__ void shade_pixel_sorted(const FrameArgs& a, float* wl
             KernArgs* kl = kernargs();
             float ts;
             uint32_t is;
-            occ = walk<false, kChunk, true, kStats>(S, o0, o1, o2, kl->L[0], kl->L[1], kl->L[2], 0.0f,
-                                                    INFINITY, ts, is, n_nodes, n_prims,
-                                                    static_cast<uint2*>(stk), true, bs);
+            occ = walk<false, kChunk, true, kStats, true>(S, o0, o1, o2, kl->L[0], kl->L[1], kl->L[2],
+                                                          0.0f, INFINITY, ts, is, n_nodes, n_prims,
+                                                          static_cast<uint2*>(stk), true, bs);
         }
         if (has) {
             slot[sl] = make_uint2(__float_as_uint(occ ? 0.0f : lam), kernargs()->sc.albedo[idx]);
@@ -995,7 +1028,7 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
     // colours and tracing order (sort_lds_bytes)
     void* stk = reinterpret_cast<uint2*>(lds + (kSort ? 0u : kBlockThreads)) + threadIdx.x;
     float* wl = kSort ? reinterpret_cast<float*>(reinterpret_cast<uint2*>(lds) +
-                                                 stack_levels(a.sc) * kBlockThreads) +
+                                                 stack_levels(a.sc, true) * kBlockThreads) +
                             wave * (kSortWaveBytes / 4u)
                       : nullptr;
     const uint32_t tw = a.tw, th = a.th;
@@ -1379,7 +1412,7 @@ static uint32_t env_u32(const char* name, uint32_t dflt) {
     return e && *e ? static_cast<uint32_t>(strtoul(e, nullptr, 10)) : dflt;
 }
 size_t sort_lds_bytes(const FrameArgs& a) {
-    return static_cast<size_t>(stack_levels(a.sc)) * kBlockThreads * sizeof(uint2) +
+    return static_cast<size_t>(stack_levels(a.sc, true)) * kBlockThreads * sizeof(uint2) +
            (kBlockThreads / 64) * kSortWaveBytes;
 }
 static bool sorted_rounds(const FrameArgs& a) {

@@ -19,7 +19,7 @@ import pytest
 import raytracingstudy_amd as rt
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-import ab_variant_check as vc  # noqa: E402
+import variant_check as vc  # noqa: E402
 
 
 def test_removed_variants_are_refused():
