@@ -77,7 +77,8 @@ def test_variants_independent_of_pad(gpu, oracle, case):
     (30000, 70, 45, 256, None, False),   # four rounds (C5's shape), edge pixels
     (30000, 70, 45, 192, None, True),    # three rounds, packed tiles with off-image pixels
     (30000, 33, 20, 100, None, False),   # a partial second round
-    (30000, 33, 20, 128, False, False),  # no jitter: every sample in quadrant 0
+    (30000, 33, 20, 128, False, False),  # no jitter: every sample in one cell
+    (30000, 20, 10, 320, None, False),   # five rounds: past the sorted path's four (unsorted)
 ])
 def test_sorted_rounds_match_oracle(gpu, oracle, n, w, h, spp, jitter, tiles):
     """Quadrant-sorted rounds (spp 65..256): the samples are traced out of
