@@ -230,7 +230,13 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
     const float o[3] = {o0, o1, o2};
     const float d[3] = {d0, d1, d2};
     float inv[3], nog[3];
-    uint32_t mask = 0;
+    // Mirror mask packed in the cell table's index layout: field i (K bits,
+    // 1 without a table) is all ones iff axis i is mirrored, so a table
+    // index is the packed l >> (D - K) XOR mt (top - c == c ^ top for c <=
+    // top), and the descent's child mirror bits are each field's low bit.
+    const uint32_t kf = S.tab_k ? S.tab_k : 1u;
+    const uint32_t ftop = (1u << kf) - 1u;
+    uint32_t mt = 0;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const float g = (o[i] - S.rmin[i]) * S.scale[i];
@@ -240,7 +246,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         const float og = neg ? S.G - g : g;
         inv[i] = 1.0f / (a * S.scale[i]);
         nog[i] = -(og * inv[i]);
-        mask |= static_cast<uint32_t>(neg) << i;
+        mt |= neg ? ftop << (i * kf) : 0u;
     }
     // t of the grid plane at (mirrored) integer k: one FMA (oracle.c:plane)
     auto plane = [&](int i, uint32_t k) { return fmaf(static_cast<float>(k), inv[i], nog[i]); };
@@ -388,12 +394,11 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                     size = half;
                     depth += 1;
                 }
-                const uint32_t sh = D - K, top = (1u << K) - 1u;
+                const uint32_t sh = D - K;
                 // real cell coordinates: mirrored axes count from the far side
-                const uint32_t c0 = (mask & 1u) ? top - (l0 >> sh) : l0 >> sh;
-                const uint32_t c1 = (mask & 2u) ? top - (l1 >> sh) : l1 >> sh;
-                const uint32_t c2 = (mask & 4u) ? top - (l2 >> sh) : l2 >> sh;
-                const uint2 e = tab[(c2 << (2u * K)) | (c1 << K) | c0];
+                // (the XOR with mt flips every mirrored field at once)
+                const uint32_t c = ((((l2 >> sh) << K) | (l1 >> sh)) << K | (l0 >> sh)) ^ mt;
+                const uint2 e = tab[c];
                 const uint32_t kind = e.y >> kCellKindShift;
                 depth = (e.y >> kCellDepthShift) & 31u;
                 size = G >> depth;
@@ -417,7 +422,9 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 const bool b1 = plane(1, l1 + half) <= t;
                 const bool b2 = plane(2, l2 + half) <= t;
                 const uint32_t bits = (b0 ? 1u : 0u) | (b1 ? 2u : 0u) | (b2 ? 4u : 0u);
-                const uint32_t child = bits ^ mask;
+                const uint32_t mbits = (mt & 1u) | ((mt >> (kf - 1u)) & 2u) |
+                                       ((mt >> (2u * kf - 2u)) & 4u);
+                const uint32_t child = bits ^ mbits;
                 l0 += b0 ? half : 0u;
                 l1 += b1 ? half : 0u;
                 l2 += b2 ? half : 0u;

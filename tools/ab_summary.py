@@ -1,0 +1,30 @@
+#!/usr/bin/env python3
+"""Summarise a tools/ab_libs2.sh log: per (config, library) the per-process
+kernel medians and their median, plus each library's change against the first.
+
+    python tools/ab_summary.py gpurun_out/r03/mt_ab.log
+"""
+import collections
+import json
+import statistics
+import sys
+
+
+def main(path):
+    runs = collections.defaultdict(list)
+    libs = []
+    for line in open(path):
+        lib, cfg, js = line.split(" ", 2)
+        if lib not in libs:
+            libs.append(lib)
+        for v in json.loads(js).values():
+            runs[(cfg, lib)].append(v["ms_median"])
+    for cfg in sorted({c for c, _ in runs}):
+        base = statistics.median(runs[(cfg, libs[0])])
+        for lib in libs:
+            m = statistics.median(runs[(cfg, lib)])
+            print(f"{cfg:4s} {lib:10s} {m:8.3f} ms  {100 * (m / base - 1):+5.1f}%  {runs[(cfg, lib)]}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -1,13 +1,27 @@
 #!/usr/bin/env bash
-# shadow-phase cost, walk block stats, bench tile-path checks after the pipeline refactor
+# Round-3 check on one GPU box after a kernel change: GPU suite, C3 + C5
+# profiles merged into one config-keyed summary (profiles/pmc_latest.json's
+# shape), then the bench reading that summary.
+# usage: bash tools/gpu_r03b.sh <tag>
 set -o pipefail
-mkdir -p gpurun_out/r03
-timeout -k 10 240 python -u tools/phase_cost.py --configs c3,c5,c5d > gpurun_out/r03/phase_cost.log 2>&1
-echo "phase rc=$?"
-RT_AMD_LIB=$PWD/abl/librt_bstats.so timeout -k 10 200 python -u tools/block_stats.py --configs c3,c5 > gpurun_out/r03/block_stats.log 2>&1
-echo "bstats rc=$?"
-timeout -k 10 200 python -u bench.py --tiles --steps 30 --secondary= --cpu-baseline off > gpurun_out/r03/bench_tiles.json 2>&1
-echo "tiles rc=$?"
-timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
-    bench.py --gpus 2 --backend gloo --same-device --steps 10 --warmup 2 --secondary= --cpu-baseline off > gpurun_out/r03/bench_gloo2.json 2>&1
-echo "gloo2 rc=$?"
+TAG=${1:-r03b}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
+    -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
+rc=$?
+echo "pytest rc=$rc"
+tail -3 "$OUT/pytest_gpu.log"
+[ $rc -eq 0 ] || exit $rc
+bash tools/profile.sh "${TAG}_c3" c3 5 && bash tools/profile.sh "${TAG}_c5" c5 3 &&
+python3 - "$TAG" <<'EOF' &&
+import json, sys
+tag = sys.argv[1]
+m = {c: json.load(open(f"gpurun_out/prof_{tag}_{c}/pmc_summary.json")) for c in ("c3", "c5")}
+json.dump(m, open(f"gpurun_out/{tag}/pmc_merged.json", "w"), indent=1)
+EOF
+timeout -k 10 300 python -u bench.py --pmc "$OUT/pmc_merged.json" > "$OUT/bench.json" 2> "$OUT/bench.err"
+rc=$?
+echo "bench rc=$rc"
+cat "$OUT/bench.json"
+exit $rc
