@@ -145,6 +145,11 @@ def roofline(kern_ms: float, touched_bytes: float, pmc, simds: int, pmc_path: st
         SIMD-32 for 2 cycles, MI355X_MICROARCH.md "Wave scheduling");
       * hbm: PMC HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950
         correction) over the live kernel time, against 8 TB/s;
+      * vmem_return: PMC TD_TD_BUSY_sum per CU-cycle (profile pass 5), the
+        texture-data unit that returns every vector load's 64 lanes of data
+        to VGPRs; a wave-wide dwordx4 sphere load returns 1 KB even when all
+        lanes read one sphere.  TA busy and the TD cycles stalled on the L1
+        ride along (a stalled cycle counts as busy);
       * l2: SURVEY 8d D4 algorithmic bytes (node + sphere records touched per
         ray) against the L2s' aggregate bandwidth.  Those bytes are served by
         L1/L2 (the scene is cache-resident), never by HBM, so they are never
@@ -178,6 +183,16 @@ def roofline(kern_ms: float, touched_bytes: float, pmc, simds: int, pmc_path: st
                                      "branch_per_launch": sq.get("SQ_INSTS_BRANCH"),
                                      "source": src + ": SQ_INSTS_SALU + SQ_INSTS_BRANCH vs 1 per "
                                                      "CU-cycle (tools/scalar_peak.hip)"}
+        if pmc.get("td_busy_frac") is not None and clock:
+            peak = simds / 4 * clock
+            frac = pmc["td_busy_frac"]
+            roofs["vmem_return"] = {
+                "achieved": round(frac * peak, 2), "peak": round(peak, 2),
+                "unit": "G TD-busy CU-cycles/s", "frac": round(frac, 4),
+                "ta_busy_frac": round(pmc.get("ta_busy_frac", 0.0), 4),
+                "td_tc_stall_frac": round(pmc.get("td_tc_stall_frac", 0.0), 4),
+                "source": src + ": TD_TD_BUSY_sum, TA_TA_BUSY_sum, TD_TC_STALL_sum per "
+                                "CU-cycle (GRBM_GUI_ACTIVE of the same pass)"}
         if traffic:
             rate = traffic / secs / 1e9
             roofs["hbm"] = {"achieved": round(rate, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -29,13 +29,29 @@ def test_valu_issue_is_the_bound_when_hbm_traffic_is_tiny():
     r = bench.roofline(kern_ms, touched, pmc, SIMDS)
     assert r["frac"] is not None and 0 < r["frac"] <= 1.0
     assert r["traffic"] / touched < 0.01
-    # the issue roofs bind (scalar pipe or VALU), never HBM
-    assert r["bound"] in ("scalar_issue", "valu_issue")
+    # an issue roof (scalar pipe or VALU) or the vector-memory return path
+    # binds, never HBM
+    assert r["bound"] in ("scalar_issue", "valu_issue", "vmem_return")
     v = r["roofs"]["valu_issue"]
     insts = pmc["sq"]["SQ_INSTS_VALU"]
     peak = SIMDS * pmc["effective_clock_ghz"] / 2.0  # G wave-instructions / s
     assert v["frac"] == pytest.approx(insts / (kern_ms / 1e3) / 1e9 / peak, rel=1e-3)
     assert all(x["frac"] <= 1.0 for k, x in r["roofs"].items() if k == r["bound"])
+
+
+def test_vmem_return_roof_from_td_busy():
+    pmc = dict(_pmc(), td_busy_frac=0.9, ta_busy_frac=0.8, td_tc_stall_frac=0.1)
+    r = bench.roofline(pmc["scene_kernel_avg_ns"] / 1e6, 182.19e9, pmc, SIMDS)
+    v = r["roofs"]["vmem_return"]
+    assert v["frac"] == pytest.approx(0.9)
+    assert v["peak"] == pytest.approx(SIMDS / 4 * pmc["effective_clock_ghz"], rel=1e-3)
+    assert v["achieved"] == pytest.approx(0.9 * v["peak"], rel=1e-3)
+    assert v["ta_busy_frac"] == pytest.approx(0.8) and v["td_tc_stall_frac"] == pytest.approx(0.1)
+    valid = {k: x["frac"] for k, x in r["roofs"].items() if x["frac"] <= 1.0}
+    assert r["bound"] == max(valid, key=valid.get)
+    # a summary without the TA/TD pass has no such roof
+    q = {k: x for k, x in _pmc().items() if k not in ("td_busy_frac", "ta_busy_frac", "td_tc_stall_frac")}
+    assert "vmem_return" not in bench.roofline(q["scene_kernel_avg_ns"] / 1e6, 1e9, q, SIMDS)["roofs"]
 
 
 def test_over_unity_roofs_are_never_chosen():

@@ -108,6 +108,16 @@ def main():
             # per CU-cycle (256 CUs, GRBM_GUI_ACTIVE summed over 8 XCDs)
             sc = sq["SQ_INSTS_SALU"][0] + sq.get("SQ_INSTS_BRANCH", (0, 0))[0]
             res["scalar_per_cu_cycle"] = sc / 256.0 / (gui / 8.0)
+    vm = counters(os.path.join(root, "vmem"))
+    vgui = vm.get("GRBM_GUI_ACTIVE", (0, 0))[0]
+    if vm.get("TD_TD_BUSY_sum") and vgui:
+        # busy cycles summed over the 256 CUs' TA / TD units, against the
+        # CU cycles of the same pass (GRBM_GUI_ACTIVE summed over 8 XCDs)
+        cu_cycles = 256.0 * vgui / 8.0
+        res["vmem"] = {k: v[0] for k, v in vm.items()}
+        res["td_busy_frac"] = vm["TD_TD_BUSY_sum"][0] / cu_cycles
+        res["ta_busy_frac"] = vm.get("TA_TA_BUSY_sum", (0, 0))[0] / cu_cycles
+        res["td_tc_stall_frac"] = vm.get("TD_TC_STALL_sum", (0, 0))[0] / cu_cycles
     print(json.dumps(res, indent=1))
 
 

@@ -5,6 +5,8 @@
 #   3. rocprofv3 --pmc WRITE_SIZE        (own pass)
 #   4. rocprofv3 --pmc SQ_WAVES,SQ_INSTS_VALU,SQ_ACTIVE_INST_VALU,SQ_WAVE_CYCLES,SQ_INSTS_SALU,
 #      SQ_INSTS_BRANCH,SQ_THREAD_CYCLES_VALU,SQ_WAIT_ANY,GRBM_GUI_ACTIVE (8 SQ + 1 GRBM)
+#   5. rocprofv3 --pmc TA_TA_BUSY_sum,TD_TD_BUSY_sum,TD_TC_STALL_sum,GRBM_GUI_ACTIVE
+#      (the vector-memory return path: 1 TA + 2 TD + 1 GRBM)
 # then tools/pmc_traffic.py -> gpurun_out/prof_<tag>/pmc_summary.json
 # Every GPU step has its own time limit and the steps are chained with &&.
 set -o pipefail
@@ -26,6 +28,9 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d "$OUT/wri
 timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_THREAD_CYCLES_VALU SQ_WAIT_ANY GRBM_GUI_ACTIVE -T \
     --output-format csv -d "$OUT/sq" -o run --kernel-include-regex scene_kernel \
     -- python3 $BENCH > "$OUT/sq.log" 2>&1 &&
+timeout -k 10 400 rocprofv3 --pmc TA_TA_BUSY_sum TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE -T \
+    --output-format csv -d "$OUT/vmem" -o run --kernel-include-regex scene_kernel \
+    -- python3 $BENCH > "$OUT/vmem.log" 2>&1 &&
 cd "$ROOT" && python3 tools/pmc_traffic.py "$OUT" "$CFG" > "$OUT/pmc_summary.json"
 rc=$?
 echo "profile rc=$rc"
