@@ -15,7 +15,12 @@ not its f32 operation order:
   the product's generator (bit-exact: the spec fixes every f32 step);
 * small frames rendered by brute force in float64 against the oracle's f32
   frames: equal within 1e-4 except where f32 and f64 disagree about a
-  silhouette or a shadow edge (a small share of pixels, bounded below).
+  silhouette or a shadow edge (a small share of pixels, bounded below);
+* the octree build (root growth, f64 closed-box overlap with its margin, the
+  split rule, breadth-first record layout), restated as a level-by-level
+  numpy queue, against the oracle's recursive C build record for record,
+  with mutants of the restatement (child bits swapped, no margin, another
+  leaf capacity) shown to differ.
 """
 from __future__ import annotations
 
@@ -303,3 +308,132 @@ def test_compat_1080p_matches_float64_spec(oracle, seed):
     assert diff.sum() <= near.sum() and near.mean() < 0.01, (int(diff.sum()), float(near.mean()))
     print(f"seed {seed}: {int(diff.sum())} differing pixels, all within the "
           f"{int(near.sum())} near-boundary pixels of {w * h}")
+
+
+def spec_octree(sp, root_min, root_max, max_depth, leaf_capacity, mutant=None):
+    """DESIGN §2.2 "Octree build", restated level by level (a breadth-first
+    queue over numpy index arrays; the oracle recurses in C and renumbers
+    afterwards), emitted in the product's record layout: slot = breadth-first
+    position; internal {first child slot, valid | leaf mask << 8}, children in
+    child order (bit 0 x, bit 1 y, bit 2 z); leaf {list offset, count}, lists
+    ascending and laid out in slot order.  Returns (nodes (n, 2), prim_idx,
+    root_min, root_max) with the root grown as the spec says."""
+    sp = np.asarray(sp, np.float32).reshape(-1, 4)
+    c64 = sp[:, :3].astype(np.float64)
+    r64 = sp[:, 3].astype(np.float64)
+    cfg_lo = np.asarray(root_min, np.float32).astype(np.float64)
+    cfg_hi = np.asarray(root_max, np.float32).astype(np.float64)
+    # the configured box, grown where some sphere's AABB leaves it, by 1e-6 x
+    # the configured box's largest extent, rounded to f32
+    um = float((cfg_hi - cfg_lo).max())
+    lo = cfg_lo.copy()
+    hi = cfg_hi.copy()
+    if len(sp):
+        lo = np.minimum(lo, (c64 - r64[:, None]).min(0))
+        hi = np.maximum(hi, (c64 + r64[:, None]).max(0))
+    rmin = np.where(lo < cfg_lo, (lo - 1e-6 * um).astype(np.float32), cfg_lo.astype(np.float32))
+    rmax = np.where(hi > cfg_hi, (hi + 1e-6 * um).astype(np.float32), cfg_hi.astype(np.float32))
+    base = rmin.astype(np.float64)
+    ext = rmax.astype(np.float64) - base
+    margin = 1e-6 * float(ext.max())
+
+    def overlapping(idx, depth, cell):
+        """Members of idx whose centre lies within r + margin of the closed
+        cell box (squared distances summed x, y, z in f64)."""
+        cells = float(1 << depth)
+        blo = base + ext * (np.asarray(cell, np.float64) / cells)
+        bhi = base + ext * ((np.asarray(cell, np.float64) + 1.0) / cells)
+        cc = c64[idx]
+        e = np.where(cc < blo, blo - cc, np.where(cc > bhi, cc - bhi, 0.0))
+        d2 = e[:, 0] * e[:, 0] + e[:, 1] * e[:, 1] + e[:, 2] * e[:, 2]
+        rr = r64[idx] + (0.0 if mutant == "no_margin" else margin)
+        if mutant == "open_box":
+            return idx[d2 < rr * rr]
+        return idx[d2 <= rr * rr]
+
+    def is_leaf(members, depth):
+        return len(members) <= leaf_capacity or depth >= max_depth
+
+    root = overlapping(np.arange(len(sp)), 0, (0, 0, 0))
+    queue = [(0, (0, 0, 0), root)]
+    nodes, prims = [], []
+    head = 0
+    while head < len(queue):
+        depth, cell, members = queue[head]
+        head += 1
+        if is_leaf(members, depth):
+            nodes.append((len(prims), len(members)))
+            prims.extend(int(i) for i in members)
+            continue
+        first, valid, leafm = len(queue), 0, 0
+        for ch in range(8):
+            bx, by, bz = ch & 1, (ch >> 1) & 1, (ch >> 2) & 1
+            if mutant == "z_fastest":
+                bx, bz = bz, bx
+            cc = (2 * cell[0] + bx, 2 * cell[1] + by, 2 * cell[2] + bz)
+            sub = overlapping(members, depth + 1, cc)
+            if not len(sub):
+                continue
+            valid |= 1 << ch
+            if is_leaf(sub, depth + 1):
+                leafm |= 1 << ch
+            queue.append((depth + 1, cc, sub))
+        nodes.append((first, valid | (leafm << 8)))
+    return (np.asarray(nodes, np.uint32).reshape(-1, 2), np.asarray(prims, np.uint32),
+            rmin, rmax)
+
+
+@pytest.mark.parametrize("case,n,depth,cap", [
+    ("uniform", 400, 5, 8), ("uniform", 3000, 6, 8), ("uniform", 3000, 4, 2),
+    ("clustered", 2000, 7, 8), ("protruding", 300, 5, 4), ("uniform", 1, 7, 8)])
+def test_octree_matches_spec_build(oracle, case, n, depth, cap):
+    """The oracle's tree, record for record, against the spec's build restated
+    here: root growth, f64 closed-box overlap with the margin, split rule,
+    empty children dropped, breadth-first slots, ascending leaf lists."""
+    if case == "clustered":
+        sp, al = rt.configs.clustered_spheres(n, SEED)
+    else:
+        sp, al = spec_spheres(n)
+    sp = np.asarray(sp, np.float32).reshape(-1, 4).copy()
+    if case == "protruding":
+        # some spheres leave the configured box on every side: the root grows
+        sp[::7, :3] = sp[::7, :3] * np.float32(1.3) - np.float32(0.2)
+    nodes, prims, rmin, rmax = spec_octree(sp, (0, 0, 0), (1.28, 1.28, 1.28), depth, cap)
+    sc = oracle.Scene(sp, al, max_depth=depth, leaf_capacity=cap)
+    o_nodes, o_prims = sc.export_bfs()
+    o_min, o_max = sc.root()
+    assert np.array_equal(o_min, rmin) and np.array_equal(o_max, rmax)
+    assert nodes.shape == o_nodes.shape and np.array_equal(nodes, o_nodes)
+    assert np.array_equal(prims, o_prims)
+    if case == "protruding":
+        assert (rmin < 0).all() and (rmax > np.float32(1.28)).all()
+    if n > cap:
+        assert len(nodes) > 1
+
+
+@pytest.mark.parametrize("mutant", ["z_fastest", "no_margin", "cap"])
+def test_octree_spec_check_catches_mutants(oracle, mutant):
+    """The comparison above has teeth: a spec restated with the child bits
+    swapped, without the overlap margin, or with another leaf capacity builds
+    a different tree for some scene."""
+    diffs = 0
+    for n, depth in ((400, 5), (3000, 6)):
+        sp, al = spec_spheres(n)
+        sp = np.asarray(sp, np.float32).reshape(-1, 4)
+        # every 5th sphere just clear of the root's x mid-plane, by less than
+        # the overlap margin (1e-6 x 1.28): only the margin puts it in the
+        # left half too
+        if mutant == "no_margin":
+            sp = sp.copy()
+            # inside the configured box, so the root (and its mid-plane) is that box's
+            sp[:, :3] = np.float32(0.1) + sp[:, :3] * np.float32(1.08 / 1.28)
+            sp[::5, 0] = np.float32(0.64) + sp[::5, 3] + np.float32(5e-7)
+        cap = 8
+        nodes, prims, _, _ = spec_octree(sp, (0, 0, 0), (1.28, 1.28, 1.28), depth,
+                                         9 if mutant == "cap" else cap,
+                                         mutant=None if mutant == "cap" else mutant)
+        o_nodes, o_prims = oracle.Scene(sp, al, max_depth=depth, leaf_capacity=cap).export_bfs()
+        same = nodes.shape == o_nodes.shape and np.array_equal(nodes, o_nodes) and \
+            np.array_equal(prims, o_prims)
+        diffs += not same
+    assert diffs > 0
