@@ -20,7 +20,13 @@ not its f32 operation order:
   split rule, breadth-first record layout), restated as a level-by-level
   numpy queue, against the oracle's recursive C build record for record,
   with mutants of the restatement (child bits swapped, no margin, another
-  leaf capacity) shown to differ.
+  leaf capacity) shown to differ;
+* the walk and its work counters, restated as a recursive front-to-back
+  descent over that independent tree in exact f32 (every fmaf rounded once
+  through rationals), against the oracle's stack walk: the same hit, t,
+  sphere, nodes_visited and prims_tested on every nearest and any-hit ray,
+  with mutants (popped records counted again, leaf lists reversed) shown
+  to differ.
 """
 from __future__ import annotations
 
@@ -436,4 +442,236 @@ def test_octree_spec_check_catches_mutants(oracle, mutant):
         same = nodes.shape == o_nodes.shape and np.array_equal(nodes, o_nodes) and \
             np.array_equal(prims, o_prims)
         diffs += not same
+    assert diffs > 0
+
+
+# ---- the walk, restated recursively in exact f32 -----------------------------
+
+_F = np.float32
+
+
+def _round_f32(q):
+    """A rational to the nearest float32, ties to even (one rounding)."""
+    from fractions import Fraction
+    x = _F(float(q))  # may be off by one step after the double rounding
+    best = x
+    for y in (np.nextafter(x, _F(-np.inf)), np.nextafter(x, _F(np.inf))):
+        dy, db = abs(Fraction(float(y)) - q), abs(Fraction(float(best)) - q)
+        if dy < db or (dy == db and int(y.view(np.uint32)) & 1 == 0):
+            best = y
+    return best
+
+
+def _fma(a, b, c):
+    """fmaf: a * b + c rounded once (Python 3.10 has no math.fma)."""
+    from fractions import Fraction
+    return _round_f32(Fraction(float(a)) * Fraction(float(b)) + Fraction(float(c)))
+
+
+def _isect(o, d, s, tmin, tmax):
+    """DESIGN §2.2 "Ray–sphere" in f32: (accepted, t)."""
+    oc = [_F(o[i] - s[i]) for i in range(3)]
+    b = _fma(oc[2], d[2], _fma(oc[1], d[1], _F(oc[0] * d[0])))
+    q = [_fma(-b, d[i], oc[i]) for i in range(3)]
+    qq = _fma(q[2], q[2], _fma(q[1], q[1], _F(q[0] * q[0])))
+    h = _fma(s[3], s[3], -qq)
+    if h < 0:
+        return False, None
+    sq = np.sqrt(h)
+    t = _F(-b - sq)
+    if not t > tmin:
+        t = _F(-b + sq)
+    if not (t > tmin) or not (t < tmax):
+        return False, None
+    return True, t
+
+
+def spec_walk(tree, sp, o, d, tmin=0.0, tmax=np.inf, any_hit=False, mutant=None):
+    """DESIGN §2.2 "Octree walk" and "Counters", restated as a recursive
+    front-to-back descent over the spec tree (the oracle keeps an explicit
+    stack and pops to the common ancestor by the highest flipped bit).  f32
+    throughout, every fmaf rounded once.  -> (hit, t, index, nodes, prims)."""
+    nodes_rec, prims, rmin, rmax = tree
+    D = tree_depth = int(spec_walk.depth)
+    G = 1 << D
+    Gf = _F(G)
+    o = [_F(v) for v in o]
+    d = [_F(v) for v in d]
+    tmin, tmax = _F(tmin), _F(tmax)
+    scale = [_F(Gf / _F(rmax[i] - rmin[i])) for i in range(3)]
+    inv, nog, mask = [], [], 0
+    for i in range(3):
+        g = _F(_F(o[i] - rmin[i]) * scale[i])
+        neg = d[i] < 0
+        a = abs(d[i])
+        if a < _F(1e-20):
+            a = _F(1e-20)
+        og = _F(Gf - g) if neg else g
+        iv = _F(_F(1.0) / _F(a * scale[i]))
+        inv.append(iv)
+        nog.append(-_F(og * iv))
+        mask |= int(neg) << i
+
+    def plane(i, k):
+        return _fma(_F(k), inv[i], nog[i])
+
+    t0, t1 = plane(0, 0), plane(0, G)
+    for i in (1, 2):
+        a0, a1 = plane(i, 0), plane(i, G)
+        if a0 > t0:
+            t0 = a0
+        if a1 < t1:
+            t1 = a1
+    if t0 < tmin:
+        t0 = tmin
+    if t1 > tmax:
+        t1 = tmax
+    if not t0 < t1:
+        return False, None, None, 0, 0
+    st = {"nodes": 1, "prims": 0, "best_t": tmax, "best": None, "hit": None}
+
+    def leaf(slot):
+        off, cnt = (int(v) for v in nodes_rec[slot])
+        for j in (range(cnt - 1, -1, -1) if mutant == "desc" else range(cnt)):
+            idx = int(prims[off + j])
+            st["prims"] += 1
+            ok, t = _isect(o, d, sp[idx], tmin, tmax)
+            if ok:
+                if any_hit:
+                    st["hit"] = (t, idx)
+                    return True
+                if t < st["best_t"] or (t == st["best_t"] and idx < st["best"]):
+                    st["best_t"], st["best"] = t, idx
+        return False
+
+    STOP = object()
+
+    def run(slot, depth, c, t):
+        """Internal node `slot` at `depth`, mirrored cell coords c, entered at
+        t.  Returns STOP, or (t, stepped coords, their depth) once the walk
+        leaves this node's cell."""
+        rx, ry = (int(v) for v in nodes_rec[slot])
+        valid, leafm = ry & 0xFF, (ry >> 8) & 0xFF
+        while True:
+            half = G >> (depth + 1)
+            bits = 0
+            for i in range(3):
+                if plane(i, (2 * c[i] + 1) * half) <= t:
+                    bits |= 1 << i
+            cc = [2 * c[i] + ((bits >> i) & 1) for i in range(3)]
+            child = bits ^ mask
+            if valid & (1 << child):
+                st["nodes"] += 1
+                cs = rx + bin(valid & ((1 << child) - 1)).count("1")
+                if not leafm & (1 << child):
+                    r = run(cs, depth + 1, cc, t)
+                    if r is STOP:
+                        return STOP
+                    t, cl, lv = r
+                    if [x >> (lv - depth) for x in cl] != list(c):
+                        return r
+                    if mutant == "reread":
+                        st["nodes"] += 1  # the spec reads no popped record again
+                    continue
+                if leaf(cs):
+                    return STOP
+            # leave the leaf / empty child cc at depth + 1
+            size = G >> (depth + 1)
+            e = [plane(i, (cc[i] + 1) * size) for i in range(3)]
+            tx = e[0] if e[0] < e[1] else e[1]
+            tx = tx if tx < e[2] else e[2]
+            if st["best_t"] < tx or tx >= t1:
+                return STOP
+            cl = [cc[i] + 1 if e[i] == tx else cc[i] for i in range(3)]
+            if any(cl[i] >= (1 << (depth + 1)) for i in range(3) if e[i] == tx):
+                return STOP
+            t = tx
+            if [x >> 1 for x in cl] != list(c):
+                return (t, cl, depth + 1)
+
+    rx, ry = (int(v) for v in nodes_rec[0])
+    if len(nodes_rec) == 1:  # the root is a leaf
+        if leaf(0) and any_hit:
+            return True, st["hit"][0], st["hit"][1], st["nodes"], st["prims"]
+    else:
+        run(0, 0, [0, 0, 0], t0)
+    if st["hit"] is not None:
+        return True, st["hit"][0], st["hit"][1], st["nodes"], st["prims"]
+    if st["best"] is not None:
+        return True, st["best_t"], st["best"], st["nodes"], st["prims"]
+    return False, None, None, st["nodes"], st["prims"]
+
+
+@pytest.mark.parametrize("case,n,depth,cap,n_rays", [
+    ("uniform", 400, 5, 8, 240), ("clustered", 2000, 7, 8, 160), ("uniform", 3000, 6, 2, 120)])
+def test_walk_counters_match_spec_walk(oracle, case, n, depth, cap, n_rays):
+    """Hits AND work counters of the oracle's walk against the spec's walk
+    restated here over the spec's own tree: nearest rays from a camera and
+    from random points in random directions (axis-parallel ones included),
+    and any-hit shadow rays from the hits toward the light."""
+    if case == "clustered":
+        sp, al = rt.configs.clustered_spheres(n, SEED)
+    else:
+        sp, al = spec_spheres(n)
+    sp = np.asarray(sp, np.float32).reshape(-1, 4)
+    tree = spec_octree(sp, (0, 0, 0), (1.28, 1.28, 1.28), depth, cap)
+    spec_walk.depth = depth
+    sc = oracle.Scene(sp, al, max_depth=depth, leaf_capacity=cap)
+    rng = np.random.default_rng(n + depth)
+    rays = []
+    eye = np.array([0.64, 0.64, 3.0], np.float32)
+    for _ in range(n_rays // 2):
+        tgt = rng.uniform(0.0, 1.28, 3).astype(np.float32)
+        rays.append((eye, (tgt - eye).astype(np.float32)))
+    for k in range(n_rays - n_rays // 2):
+        o = rng.uniform(-0.2, 1.5, 3).astype(np.float32)
+        dv = rng.normal(size=3).astype(np.float32)
+        if k % 5 == 0:
+            dv[rng.integers(3)] = 0.0  # parallel to a cell plane
+        rays.append((o, dv))
+    # the spec's rays are unit length (the discriminant assumes it)
+    rays = [(o, (dv / np.float32(np.sqrt(np.float32(dv @ dv)))).astype(np.float32)) for o, dv in rays]
+    light = -np.array([1.0, 1.0, -1.0], np.float32) / np.float32(np.sqrt(3.0))
+    n_hit = n_shadow = 0
+    for o, dv in rays:
+        hit, t, idx, nodes, prims = spec_walk(tree, sp, o, dv)
+        oh, ot, oi, cnt = sc.trace(o, dv)
+        assert (hit, nodes, prims) == (oh, int(cnt[2]), int(cnt[3]))
+        if not hit:
+            continue
+        n_hit += 1
+        assert (np.float32(t), idx) == (np.float32(ot), oi)
+        # an any-hit ray from just off the surface toward the light
+        p = (o + np.float32(t) * dv).astype(np.float32)
+        so = (p + np.float32(1e-3) * light).astype(np.float32)
+        sh, st_, si, sn, spr = spec_walk(tree, sp, so, light, any_hit=True)
+        qh, qt, qi, qc = sc.trace(so, light, any_hit=True)
+        assert (sh, sn, spr) == (qh, int(qc[2]), int(qc[3]))
+        if sh:
+            assert (np.float32(st_), si) == (np.float32(qt), qi)
+        n_shadow += 1
+    assert n_hit > n_rays // 10 and n_shadow == n_hit
+
+
+@pytest.mark.parametrize("mutant", ["reread", "desc"])
+def test_walk_spec_check_catches_mutants(oracle, mutant):
+    """The walk comparison has teeth: counting a popped record again, or
+    testing a leaf's spheres in descending order (any-hit rays then count
+    other tests), changes some counter."""
+    sp, al = spec_spheres(2000)
+    sp = np.asarray(sp, np.float32).reshape(-1, 4)
+    tree = spec_octree(sp, (0, 0, 0), (1.28, 1.28, 1.28), 6, 4)
+    spec_walk.depth = 6
+    sc = oracle.Scene(sp, al, max_depth=6, leaf_capacity=4)
+    rng = np.random.default_rng(7)
+    light = -np.array([1.0, 1.0, -1.0], np.float32) / np.float32(np.sqrt(3.0))
+    diffs = 0
+    for _ in range(40):
+        o = rng.uniform(0.0, 1.28, 3).astype(np.float32)
+        dv = rng.normal(size=3).astype(np.float32)
+        dv = (dv / np.float32(np.sqrt(np.float32(dv @ dv)))).astype(np.float32)
+        for dd, anyh in ((dv, False), (light, True)):
+            _, _, _, nodes, prims = spec_walk(tree, sp, o, dd, any_hit=anyh, mutant=mutant)
+            _, _, _, cnt = sc.trace(o, dd, any_hit=anyh)
+            diffs += (nodes, prims) != (int(cnt[2]), int(cnt[3]))
     assert diffs > 0
