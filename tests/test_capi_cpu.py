@@ -145,5 +145,5 @@ def test_committed_pmc_summary_feeds_the_bench_roofline():
     assert r["bound"] in ("scalar_issue", "valu_issue", "vmem_return") and 0.0 < r["frac"] <= 1.0
     assert "scalar_issue" in r["roofs"] and "valu_issue" in r["roofs"]
     assert r["traffic"] and r["traffic"] > 0
-    assert bench.load_pmc(path, "c2", 1, kernel_source_id())[0] is None
+    assert bench.load_pmc(path, "c4", 1, kernel_source_id())[0] is None  # not profiled
     assert bench.load_pmc(path, "c3", 2, kernel_source_id())[0] is None
