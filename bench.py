@@ -86,7 +86,7 @@ def cpu_baseline(cfg, K, pose, target_s: float) -> dict:
     import raytracingstudy_amd as rt
 
     sp, al = rt.configs.scene_spheres(cfg, rt.SEED)
-    sc = oracle.Scene(sp, al, max_depth=cfg.max_depth)
+    sc = oracle.Scene(sp, al, max_depth=cfg.max_depth, leaf_capacity=cfg.leaf_capacity)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or oracle.max_threads()
     # calibrate on one row, then take every step-th row for ~target_s seconds
     t = time.perf_counter()
@@ -115,10 +115,11 @@ def cpu_baseline(cfg, K, pose, target_s: float) -> dict:
                             "sample": f"every {s1}th row ({rays1} rays) in {el1:.2f} s"}}
 
 
-def load_pmc(path: str, cfg_name: str, world: int, src_id: str):
+def load_pmc(path: str, cfg_name: str, world: int, src_id: str, leaf_capacity: int = 8):
     """The committed PMC summary (tools/pmc_traffic.py output) for this config
     and GPU count, or (None, reason) when it is missing, taken on another
-    config, or stamped with other kernel sources than this build's."""
+    config or octree leaf capacity, or stamped with other kernel sources than
+    this build's."""
     try:
         with open(path) as f:
             pm = json.load(f)
@@ -130,6 +131,9 @@ def load_pmc(path: str, cfg_name: str, world: int, src_id: str):
     if ent.get("kernel_source_id") != src_id:
         return None, (f"PMC summary stamped {ent.get('kernel_source_id')!r}, kernel sources are "
                       f"{src_id!r}: stale, not used")
+    if ent.get("leaf_capacity", 8) != leaf_capacity:
+        return None, (f"PMC summary taken at leaf capacity {ent.get('leaf_capacity', 8)}, "
+                      f"the config builds {leaf_capacity}: stale, not used")
     return ent, "ok"
 
 
@@ -230,7 +234,7 @@ def secondary_config(rt, torch, name: str, dev, stream, steps: int = 3, pmc_path
     try:
         r2.resize(c.width, c.height)
         r2.setPosition(scene_pose())
-        info = r2.set_scene(sp, al, max_depth=c.max_depth)
+        info = r2.set_scene(sp, al, max_depth=c.max_depth, leaf_capacity=c.leaf_capacity)
         st = r2.render(None, stream.cuda_stream, stats=True)
         rays = st.primary_rays + st.shadow_rays
         ms = []
@@ -245,7 +249,8 @@ def secondary_config(rt, torch, name: str, dev, stream, steps: int = 3, pmc_path
         k = float(np.median(ms))
         alg = (st.nodes_visited * NODE_BYTES + st.prims_tested * PRIM_BYTES +
                c.width * c.height * PIXEL_BYTES)
-        pmc, note = load_pmc(pmc_path, name, 1, rt._lib.kernel_source_id()) if pmc_path else (None, "")
+        pmc, note = (load_pmc(pmc_path, name, 1, rt._lib.kernel_source_id(), c.leaf_capacity)
+                     if pmc_path else (None, ""))
         roof = roofline(k, alg, pmc, simds, pmc_path, note)
         roof["time_ms"] = round(k, 4)
         roof["per_ray"] = {"nodes": st.nodes_visited / rays, "prims": st.prims_tested / rays}
@@ -296,7 +301,7 @@ def main():
     r.resize(cfg.width, cfg.height)
     pose = scene_pose()
     r.setPosition(pose)
-    info = r.set_scene(sp, al, max_depth=cfg.max_depth, leaf_capacity=rt.configs.LEAF_CAPACITY)
+    info = r.set_scene(sp, al, max_depth=cfg.max_depth, leaf_capacity=cfg.leaf_capacity)
     _, K = r.camera()
 
     dev = torch.device("cuda", local)
@@ -311,7 +316,7 @@ def main():
                                variant=args.variant)
         r2.resize(cfg.width, cfg.height)
         r2.setPosition(pose)
-        r2.set_scene(sp, al, max_depth=cfg.max_depth, leaf_capacity=rt.configs.LEAF_CAPACITY)
+        r2.set_scene(sp, al, max_depth=cfg.max_depth, leaf_capacity=cfg.leaf_capacity)
         rs.append(r2)
     # a real (non-null) stream: the kernels, the HIP events and RCCL all run on it
     if F == 1:
@@ -420,7 +425,8 @@ def main():
         pix = (W * H) if not tiled else len(my_ids) * ts * ts
         alg_bytes = float(cnt[2].item()) * NODE_BYTES + float(cnt[3].item()) * PRIM_BYTES + pix * PIXEL_BYTES
         simds = torch.cuda.get_device_properties(dev).multi_processor_count * 4
-        pmc, pmc_note = load_pmc(args.pmc, cfg.name, world, rt._lib.kernel_source_id())
+        pmc, pmc_note = load_pmc(args.pmc, cfg.name, world, rt._lib.kernel_source_id(),
+                                 cfg.leaf_capacity)
         # frames in flight overlap, so one frame's event span is not its share
         # of the GPU: price a frame per step of wall time instead
         roof_ms = kern_ms if F == 1 else elapsed / args.steps * 1e3
@@ -449,7 +455,7 @@ def main():
                 "workload": f"{cfg.name}: {cfg.note}",
                 "width": W, "height": H, "spp": cfg.spp, "n_spheres": cfg.n_spheres,
                 "octree_depth": info["max_depth"], "octree_nodes": info["n_nodes"],
-                "prim_refs": info["n_prim_refs"], "leaf_capacity": rt.configs.LEAF_CAPACITY,
+                "prim_refs": info["n_prim_refs"], "leaf_capacity": cfg.leaf_capacity,
                 "parallelism": f"tiles{ts}x{world}" if tiled else "single",
                 "frames_in_flight": F,
                 "rays_per_frame": int(rays_frame),

@@ -20,6 +20,13 @@ class RenderConfig:
     mode: str
     note: str
     scene: str = "uniform"  # sphere generator: "uniform"  or "clustered"
+    # Octree leaf capacity.  A build parameter, not part of the image: every
+    # capacity gives the same pixels (nearest hit = min t then min index;
+    # shadow = any hit), only the work counters move.  Measured in one process
+    # per config (profiles/r03/cap_ab*.log): C3 8.82 ms at 8 -> 8.61 at 12
+    # (10: 8.64, 16: 8.64, 24: 9.75; 2-6 slower), C5 54.9 -> 51.9.  C5d keeps 8:
+    # at 12 its tree stops at depth 11, and the config exists for depth 12.
+    leaf_capacity: int = 8
 
     @property
     def pixels(self) -> int:
@@ -31,11 +38,14 @@ CONFIGS = {
                        "reference-compat root box, CPU scalar loop (plumbing)"),
     "c2": RenderConfig("c2", 1920, 1080, 1, 1_000, 7, 1, "scene", "1 spp, ~1k-sphere octree"),
     "c3": RenderConfig("c3", 1920, 1080, 64, 100_000, 7, 1, "scene",
-                       "64 spp Monte-Carlo accumulate, ~100k spheres (headline)"),
+                       "64 spp Monte-Carlo accumulate, ~100k spheres (headline)",
+                       leaf_capacity=12),
     "c4": RenderConfig("c4", 3840, 2160, 64, 100_000, 7, 8, "scene",
-                       "64 spp, 100k spheres, 64x64 tiles across 8 GPUs + RCCL gather"),
+                       "64 spp, 100k spheres, 64x64 tiles across 8 GPUs + RCCL gather",
+                       leaf_capacity=12),
     "c5": RenderConfig("c5", 1920, 1080, 256, 1_000_000, 12, 1, "scene",
-                       "256 spp, 1M spheres, depth-12 octree (compaction stress)"),
+                       "256 spp, 1M spheres, depth-12 octree (compaction stress)",
+                       leaf_capacity=12),
     # C5 with a tree that actually reaches depth 12 (BASELINE config 5 "deep
     # (depth-12) octree"): uniform centres stop splitting at depth 8, so the
     # same 1M spheres are drawn around 64 clusters (clustered_spheres)
@@ -69,5 +79,5 @@ def scene_spheres(cfg: "RenderConfig", seed: int = SEED):
 
 LIGHT_DIR = (1.0, 1.0, -1.0)  # direction the light travels (normalize(1,1,-1))
 AMBIENT = 0.1
-LEAF_CAPACITY = 8
+LEAF_CAPACITY = 8  # the C-ABI default (rt_octree_params); configs may set their own
 TILE_SIZE = 64

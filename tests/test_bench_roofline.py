@@ -8,6 +8,7 @@ import pytest
 
 import bench
 from raytracingstudy_amd._lib import kernel_source_id
+import raytracingstudy_amd as rt
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PMC = os.path.join(ROOT, "profiles", "pmc_latest.json")
@@ -76,15 +77,20 @@ def test_stale_pmc_summary_is_refused(tmp_path):
     assert ent is None and "stale" in why
     pmc["kernel_source_id"] = kernel_source_id()
     p.write_text(json.dumps(pmc))
-    ent, why = bench.load_pmc(str(p), pmc["config"], 1, kernel_source_id())
+    ent, why = bench.load_pmc(str(p), pmc["config"], 1, kernel_source_id(),
+                              pmc.get("leaf_capacity", 8))
     assert ent is not None and why == "ok"
     assert bench.load_pmc(str(p), "c5", 1, kernel_source_id())[0] is None
+    # counters taken on a tree of another leaf capacity are another workload
+    ent, why = bench.load_pmc(str(p), pmc["config"], 1, kernel_source_id(),
+                              pmc.get("leaf_capacity", 8) + 4)
+    assert ent is None and "leaf capacity" in why
 
 
 def test_summary_holds_c3_and_c5_with_lane_counters():
     """the lane-utilisation counters on HEAD's kernel, for C3 and C5."""
     for cfg in ("c3", "c5"):
-        ent, why = bench.load_pmc(PMC, cfg, 1, kernel_source_id())
+        ent, why = bench.load_pmc(PMC, cfg, 1, kernel_source_id(), rt.CONFIGS[cfg].leaf_capacity)
         assert ent is not None, why
         sq = ent["sq"]
         assert ent["valu_lane_util"] == pytest.approx(

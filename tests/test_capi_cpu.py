@@ -139,7 +139,8 @@ def test_committed_pmc_summary_feeds_the_bench_roofline():
     import bench
     from raytracingstudy_amd._lib import kernel_source_id
     path = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    ent, why = bench.load_pmc(path, "c3", 1, kernel_source_id())
+    import raytracingstudy_amd as rt
+    ent, why = bench.load_pmc(path, "c3", 1, kernel_source_id(), rt.CONFIGS["c3"].leaf_capacity)
     assert ent is not None, why
     r = bench.roofline(ent["scene_kernel_avg_ns"] / 1e6, 182e9, ent, 1024)
     assert r["bound"] in ("scalar_issue", "valu_issue", "vmem_return") and 0.0 < r["frac"] <= 1.0

@@ -206,7 +206,8 @@ def test_scene_c3_rows_subsample(gpu, oracle, variant):
 def test_scene_c3_full_spp_rows(gpu, oracle, variant):
     """C3 exactly as benchmarked (1920x1080, 64 spp, 100k spheres), every 64th row."""
     img, rad, st, info, ref8, ref32, cnt, _ = _scene_pair(oracle, 100_000, 1920, 1080, 64,
-                                                           row_step=64, variant=variant)
+                                                           row_step=64, variant=variant,
+                                                           leaf=rt.CONFIGS["c3"].leaf_capacity)
     rows = np.arange(0, 1080, 64)
     assert np.array_equal(img[rows], ref8[rows])
     assert np.array_equal(rad[rows], ref32[rows])
@@ -229,14 +230,15 @@ def test_scene_c3_full_frame_on_caller_stream(gpu, oracle):
     with rt.KernelRenderer(w, h, mode="scene", spp=spp, radiance=True) as r:
         r.resize(w, h)
         r.setPosition(scene_pose())
-        r.set_scene(sp, al)
+        r.set_scene(sp, al, leaf_capacity=rt.CONFIGS["c3"].leaf_capacity)  # as benchmarked
         torch.cuda.synchronize()
         r.render(None, s.cuda_stream)   # asynchronous, caller's stream
         img = r.readback()              # no sync in between
         rad = r.readback_radiance()
         st = r.render(None, s.cuda_stream, stats=True)
         _, K = r.camera()
-    ref8, ref32, cnt = oracle.Scene(sp, al).render(w, h, scene_pose(), K, spp=spp)
+    ref8, ref32, cnt = oracle.Scene(sp, al, leaf_capacity=rt.CONFIGS["c3"].leaf_capacity).render(
+        w, h, scene_pose(), K, spp=spp)
     assert np.array_equal(img, ref8)
     assert np.array_equal(rad, ref32)
     assert np.abs(rad - ref32).max() <= TOL
@@ -273,7 +275,8 @@ def test_frames_on_two_caller_streams_are_ordered(gpu, oracle):
 def test_scene_c4_full_frame(gpu, oracle):
     """C4 (3840x2160, 64 spp, 100k spheres) over the whole frame (all 2160
     rows): RGBA8 and radiance bit-exact, all four counters equal."""
-    img, rad, st, info, ref8, ref32, cnt, _ = _scene_pair(oracle, 100_000, 3840, 2160, 64)
+    img, rad, st, info, ref8, ref32, cnt, _ = _scene_pair(oracle, 100_000, 3840, 2160, 64,
+                                                           leaf=rt.CONFIGS["c4"].leaf_capacity)
     assert np.array_equal(img, ref8)
     assert np.array_equal(rad, ref32)
     assert st.primary_rays == 3840 * 2160 * 64
@@ -284,7 +287,8 @@ def test_scene_c5_full_frame(gpu, oracle):
     """C5 (1920x1080, 256 spp, 1M spheres, depth-12 octree) over the whole
     frame: RGBA8 and radiance bit-exact, all four counters equal."""
     img, rad, st, info, ref8, ref32, cnt, oinfo = _scene_pair(oracle, 1_000_000, 1920, 1080, 256,
-                                                               depth=12)
+                                                               depth=12,
+                                                               leaf=rt.CONFIGS["c5"].leaf_capacity)
     assert (info["n_nodes"], info["n_prim_refs"]) == (oinfo["n_nodes"], oinfo["n_prim_refs"])
     assert info["cell_table_depth"] == 6
     assert np.array_equal(img, ref8)
@@ -300,7 +304,8 @@ def test_scene_c5_deep_full_frame(gpu, oracle):
     c = rt.CONFIGS["c5d"]
     sp, al = rt.configs.scene_spheres(c)
     img, rad, st, info, ref8, ref32, cnt, oinfo = _scene_pair(
-        oracle, c.n_spheres, c.width, c.height, c.spp, depth=c.max_depth, spheres=(sp, al))
+        oracle, c.n_spheres, c.width, c.height, c.spp, depth=c.max_depth, spheres=(sp, al),
+        leaf=c.leaf_capacity)
     assert info["depth_reached"] == oinfo["depth_reached"] == 12
     assert (info["n_nodes"], info["n_prim_refs"]) == (oinfo["n_nodes"], oinfo["n_prim_refs"])
     assert np.array_equal(img, ref8)

@@ -66,7 +66,11 @@ def main():
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from raytracingstudy_amd._lib import kernel_source_id
     # stamp: bench.py takes these counters only while the kernel sources match
-    res = {"config": cfg, "n_gpus": 1, "kernel_source_id": kernel_source_id()}
+    from raytracingstudy_amd.configs import CONFIGS
+    # and the octree build parameter the counters were taken at (round 3: a
+    # config's leaf capacity changes its work, not its image)
+    res = {"config": cfg, "n_gpus": 1, "kernel_source_id": kernel_source_id(),
+           "leaf_capacity": CONFIGS[cfg].leaf_capacity}
     ks = kernel_stats(os.path.join(root, "trace"))
     res["kernel_stats"] = ks
     durs = trace_durations(os.path.join(root, "trace"))

@@ -38,7 +38,7 @@ def main():
     r = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=cfg.spp, opt_off=args.opt)
     r.resize(cfg.width, cfg.height)
     r.setPosition(scene_pose())
-    r.set_scene(sp, al, max_depth=cfg.max_depth)
+    r.set_scene(sp, al, max_depth=cfg.max_depth, leaf_capacity=cfg.leaf_capacity)
     stream = torch.cuda.Stream()
     ts = rt.configs.TILE_SIZE
     tx, ty = T.tile_grid(cfg.width, cfg.height, ts)

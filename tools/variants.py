@@ -31,8 +31,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--spp", type=int, default=0, help="override spp")
     args = ap.parse_args()
-    # a variant spec is "V", "V:OPT" or "V:OPT:T" (OPT = rt_config opt bits, A/B
-    # toggles; T = cell-table depth: 0 off, 1..7, absent = chosen from the tree)
+    # a variant spec is "V", "V:OPT", "V:OPT:T" or "V:OPT:T:CAP" (OPT = rt_config
+    # opt bits, A/B toggles; T = cell-table depth: 0 off, 1..7, absent = chosen
+    # from the tree; CAP = octree leaf capacity, absent = the config's)
     variants = args.variants.split(",")
     if len(set(variants)) != len(variants):
         ap.error("--variants: each spec at most once (rounds repeat them)")
@@ -44,12 +45,14 @@ def main():
         rs = {}
         for v in variants:
             vv, _, rest = v.partition(":")
-            oo, _, tt = rest.partition(":")
+            oo, _, rest = rest.partition(":")
+            tt, _, cc = rest.partition(":")
             r = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=spp, variant=int(vv),
                                   opt_off=int(oo or 0), cell_table=int(tt) if tt else None)
             r.resize(cfg.width, cfg.height)
             r.setPosition(scene_pose())
-            info = r.set_scene(sp, al, max_depth=cfg.max_depth)
+            info = r.set_scene(sp, al, max_depth=cfg.max_depth,
+                               leaf_capacity=int(cc) if cc else cfg.leaf_capacity)
             r.cell_table_depth = info["cell_table_depth"]
             r.render(stats=True)  # warm-up
             rs[v] = r
