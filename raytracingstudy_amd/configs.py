@@ -26,6 +26,7 @@ class RenderConfig:
     # per config (profiles/r03/cap_ab*.log): C3 8.82 ms at 8 -> 8.61 at 12
     # (10: 8.64, 16: 8.64, 24: 9.75; 2-6 slower), C5 54.9 -> 51.9.  C5d keeps 8:
     # at 12 its tree stops at depth 11, and the config exists for depth 12.
+    # C2 keeps 8 too: 0.154 ms against 0.156 at 12 (c2_cap_ab.log).
     leaf_capacity: int = 8
 
     @property

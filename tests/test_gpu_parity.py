@@ -160,6 +160,19 @@ def test_scene_bit_exact(gpu, oracle, n, w, h, spp, depth, variant):
     _check_counts(st, cnt, variant)
 
 
+@pytest.mark.parametrize("leaf", [2, 12, 24])
+def test_scene_leaf_capacity(gpu, oracle, leaf):
+    """Another leaf capacity (C3/C4/C5 are benchmarked at 12): the GPU tree,
+    image and all four counters equal the oracle's at that capacity, and the
+    image equals the default capacity's."""
+    img, rad, st, info, ref8, ref32, cnt, oinfo = _scene_pair(oracle, 20000, 200, 150, 4, leaf=leaf)
+    assert (info["n_nodes"], info["n_prim_refs"]) == (oinfo["n_nodes"], oinfo["n_prim_refs"])
+    assert np.array_equal(img, ref8) and np.array_equal(rad, ref32)
+    _check_counts(st, cnt, 0)
+    img8, rad8, *_ = _scene_pair(oracle, 20000, 200, 150, 4, leaf=8)
+    assert np.array_equal(img, img8) and np.array_equal(rad, rad8)
+
+
 @pytest.mark.parametrize("cell_table", [None, 0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("n,w,h,spp,depth", [
     (1000, 160, 120, 4, 7),

@@ -129,6 +129,30 @@ def test_walk_matches_brute_force(oracle, n, depth, leaf):
                 assert (t1, i1) == (t2, i2)
 
 
+def test_leaf_capacity_changes_work_not_image(oracle):
+    """The leaf capacity is a build parameter (C3/C4/C5 are benchmarked at 12,
+    the C-ABI default is 8): any capacity gives the same pixels, since the
+    nearest hit is min t then min index over the spheres a ray meets and a
+    shadow ray only asks whether any sphere lies on it.  The work counters
+    move (fewer, larger leaves: fewer node visits, more sphere tests)."""
+    import raytracingstudy_amd as rt
+    from raytracingstudy_amd.camera import scene_pose
+    sp, al = oracle.generate_spheres(20000, SEED)
+    K = oracle.resize_intrinsic(160, 120)
+    out = {}
+    for cap in (2, 8, 12, 24):
+        sc = oracle.Scene(sp, al, max_depth=7, leaf_capacity=cap)
+        out[cap] = sc.render(160, 120, scene_pose(), K, spp=4)
+        sc.close()
+    for cap in (2, 12, 24):
+        assert np.array_equal(out[cap][0], out[8][0]) and np.array_equal(out[cap][1], out[8][1])
+        assert (out[cap][2][0], out[cap][2][1]) == (out[8][2][0], out[8][2][1])  # rays cast
+    nodes = [int(out[c][2][2]) for c in (2, 8, 12, 24)]
+    prims = [int(out[c][2][3]) for c in (2, 8, 12, 24)]
+    assert nodes == sorted(nodes, reverse=True) and prims == sorted(prims)
+    assert rt.CONFIGS["c3"].leaf_capacity == 12 and rt.CONFIGS["c5d"].leaf_capacity == 8
+
+
 def test_walk_tmax_and_grid_aligned_rays(oracle):
     sp = np.array([[0.32, 0.32, 0.32, 0.05], [0.96, 0.32, 0.32, 0.05]], np.float32)
     sc = oracle.Scene(sp, None, max_depth=7, leaf_capacity=1)
