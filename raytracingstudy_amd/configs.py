@@ -24,9 +24,10 @@ class RenderConfig:
     # capacity gives the same pixels (nearest hit = min t then min index;
     # shadow = any hit), only the work counters move.  Measured in one process
     # per config (profiles/r03/cap_ab*.log): C3 8.82 ms at 8 -> 8.61 at 12
-    # (10: 8.64, 16: 8.64, 24: 9.75; 2-6 slower), C5 54.9 -> 51.9.  C5d keeps 8:
-    # at 12 its tree stops at depth 11, and the config exists for depth 12.
-    # C2 keeps 8 too: 0.154 ms against 0.156 at 12 (c2_cap_ab.log).
+    # (10: 8.64, 16: 8.64, 24: 9.75; 2-6 slower), C5 54.9 -> 51.9.  C5d takes
+    # 10, the largest capacity whose tree still reaches depth 12 (at 11 and 12
+    # it stops at 11, and the config exists for depth 12): 26.28 -> 25.71 ms
+    # (c5d_cap.log).  C2 keeps 8: 0.154 ms against 0.156 at 12 (c2_cap_ab.log).
     leaf_capacity: int = 8
 
     @property
@@ -51,7 +52,8 @@ CONFIGS = {
     # (depth-12) octree"): uniform centres stop splitting at depth 8, so the
     # same 1M spheres are drawn around 64 clusters (clustered_spheres)
     "c5d": RenderConfig("c5d", 1920, 1080, 256, 1_000_000, 12, 1, "scene",
-                        "256 spp, 1M clustered spheres, octree reaching depth 12", "clustered"),
+                        "256 spp, 1M clustered spheres, octree reaching depth 12", "clustered",
+                        leaf_capacity=10),
 }
 
 
@@ -59,8 +61,9 @@ def clustered_spheres(n: int, seed: int = SEED, clusters: int = 64, sigma: float
     """n spheres around `clusters` Gaussian clusters (sd `sigma`) whose centres
     are uniform in [0.15, 1.13]^3, clipped to the root box; radii and albedo
     as SURVEY 8d D2 (0.02 (1000/n)^(1/3) U[0.5, 1]).  numpy PCG64 from `seed`:
-    the same arrays on every machine.  At 1M spheres the octree (leaf capacity
-    8, max depth 12) reaches depth 12: 1.77 M nodes, 5.9 M leaf references."""
+    the same arrays on every machine.  At 1M spheres the octree (max depth 12)
+    reaches depth 12 at leaf capacity 8 (1.74 M nodes, 5.8 M leaf references)
+    and 10 (1.24 M, 4.9 M; the benchmarked one), not at 11 or 12."""
     g = np.random.default_rng(seed)
     centres = g.uniform(0.15, 1.13, (clusters, 3))
     which = g.integers(0, clusters, n)

@@ -150,7 +150,7 @@ def test_leaf_capacity_changes_work_not_image(oracle):
     nodes = [int(out[c][2][2]) for c in (2, 8, 12, 24)]
     prims = [int(out[c][2][3]) for c in (2, 8, 12, 24)]
     assert nodes == sorted(nodes, reverse=True) and prims == sorted(prims)
-    assert rt.CONFIGS["c3"].leaf_capacity == 12 and rt.CONFIGS["c5d"].leaf_capacity == 8
+    assert rt.CONFIGS["c3"].leaf_capacity == 12 and rt.CONFIGS["c5d"].leaf_capacity == 10
 
 
 def test_walk_tmax_and_grid_aligned_rays(oracle):
