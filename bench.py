@@ -41,6 +41,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # SALU+branch per CU-cycle by tools/scalar_peak.hip, profiles/r02/scalar_peak.json)
 SCALAR_PER_CU_CYCLE = 1.0
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s over the 8 XCDs
+# what the TD charges one vector-memory read wave-instruction: 64 lanes x 16 B
+# (a dwordx2 or one-lane load costs what a wave-wide dwordx4 does)
+VMEM_CHARGE_BYTES = 64 * 16
 
 
 def parse():
@@ -139,29 +142,37 @@ def load_pmc(path: str, cfg_name: str, world: int, src_id: str, leaf_capacity: i
 
 def roofline(kern_ms: float, touched_bytes: float, pmc, simds: int, pmc_path: str = "",
              pmc_note: str = "") -> dict:
-    """Every roof this kernel could sit under, each computed from measured data,
-    and the binding one (largest valid fraction) on top:
-      * scalar_issue: PMC SQ_INSTS_SALU + SQ_INSTS_BRANCH per launch over the
-        live kernel time, against one scalar instruction per CU-cycle (the
-        CU's single scalar unit; the divergent walk's exec-mask bookkeeping);
-      * valu_issue: PMC SQ_INSTS_VALU per launch over the live kernel time,
-        against SIMDs x clock / 2 (a wave64 VALU instruction occupies a
-        SIMD-32 for 2 cycles, MI355X_MICROARCH.md "Wave scheduling");
-      * hbm: PMC HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950
-        correction) over the live kernel time, against 8 TB/s;
-      * vmem_return: PMC TD_TD_BUSY_sum per CU-cycle (profile pass 5), the
-        texture-data unit that returns every vector load's 64 lanes of data
-        to VGPRs; a wave-wide dwordx4 sphere load returns 1 KB even when all
-        lanes read one sphere.  TA busy and the TD cycles stalled on the L1
-        ride along (a stalled cycle counts as busy);
-      * l2: SURVEY 8d D4 algorithmic bytes (node + sphere records touched per
-        ray) against the L2s' aggregate bandwidth.  Those bytes are served by
-        L1/L2 (the scene is cache-resident), never by HBM, so they are never
-        priced against HBM.
-    A fraction > 1 is not a valid roof and is never chosen."""
+    """SURVEY 8d D3/D4's roofline of the scene kernel, plus what binds it.
+
+    Headline (`bound`, `achieved`, `peak`, `frac`): the D4 algorithmic bytes
+    (node records x 8 B + sphere records x 16 B touched, from the oracle's
+    counters which the GPU reproduces, + 4 B per pixel written) per launch
+    over the kernel time, against the peak of the level that SERVES them:
+    the L2s' aggregate ~34.5 TB/s (MI355X_MICROARCH.md "L2 (per XCD)").  The
+    scene is cache-resident, so those bytes never come from HBM:
+
+        frac = D4_bytes / kernel_s / 34.5e12          
+
+    Beside it:
+      * hbm_literal: the same bytes against HBM's 8 TB/s, as D3 literally
+        prices them.  Above 1, which proves they are not HBM-served;
+      * hbm_counter: the HBM bytes the PMC counters saw per launch
+        (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) over 8 TB/s;
+      * binding_unit: the busiest unit by the PMC counters: the texture-data
+        (TD) unit that returns vector loads to VGPRs (TD_TD_BUSY per
+        CU-cycle; a stalled cycle counts as busy), the VALU issue slots, or
+        the CU's one scalar pipe;
+      * waste: charged / algorithmic bytes, where a vector-memory read
+        wave-instruction (SQ_INSTS_VMEM_RD) is charged 64 lanes x 16 B at the
+        TD (a dwordx2 or a one-lane load costs what a dwordx4 does,
+        DESIGN.md 5.1 "What the cost is per"); waste_l1 prices the L1's
+        64-B cache accesses (TCP_TOTAL_CACHE_ACCESSES) instead.
+    `roofs` keeps every roof with its source."""
     secs = kern_ms / 1e3
     roofs = {}
     traffic = None
+    src = ""
+    clock = None
     if pmc:
         traffic = pmc.get("hbm_bytes_per_launch")
         insts = pmc.get("valu_insts_per_launch", pmc.get("sq", {}).get("SQ_INSTS_VALU"))
@@ -207,13 +218,45 @@ def roofline(kern_ms: float, touched_bytes: float, pmc, simds: int, pmc_path: st
                    "frac": round(l2 / L2_PEAK_GBS, 4), "touched_bytes_per_launch": int(touched_bytes),
                    "source": "SURVEY 8d D4 algorithmic bytes (oracle counters) vs "
                              "MI355X_MICROARCH.md L2 aggregate ~34.5 TB/s; L1/L2-served"}
-    valid = {k: v for k, v in roofs.items() if v["frac"] <= 1.0}
-    bound = max(valid, key=lambda k: valid[k]["frac"]) if valid else None
-    top = roofs[bound] if bound else {}
-    out = {"bound": bound, "achieved": top.get("achieved"), "peak": top.get("peak"),
-           "unit": top.get("unit"), "frac": top.get("frac"), "traffic": traffic,
-           "touched_bytes": int(touched_bytes),
-           "roofs": roofs}
+    top = roofs["l2"]
+    out = {"bound": "l2", "achieved": top["achieved"], "peak": top["peak"], "unit": top["unit"],
+           "frac": top["frac"], "traffic": traffic,
+           "served_by": "L1/L2: the scene is cache-resident (HBM sees the framebuffer and little else)",
+           "formula": "frac = D4 bytes per launch / kernel s / 34.5e12 B/s; D4 = nodes_visited x 8 + "
+                      "prims_tested x 16 + pixels x 4 (SURVEY 8d D4, DESIGN.md 5.2)",
+           "algorithmic_bytes": int(touched_bytes), "kernel_ms": round(kern_ms, 4),
+           "hbm_literal": {"achieved": top["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(l2 / HBM_PEAK_GBS, 4), "hbm_served": False,
+                           "note": "D4 bytes priced against HBM as SURVEY 8d D3 states it; > 1 "
+                                   "because they are served by L1/L2, not HBM"}}
+    if "hbm" in roofs:
+        h = roofs["hbm"]
+        out["hbm_counter"] = {"bytes_per_launch": h["bytes_per_launch"], "achieved": h["achieved"],
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": h["frac"],
+                              "source": h["source"]}
+    units = {k: roofs[k] for k in ("vmem_return", "valu_issue", "scalar_issue") if k in roofs
+             and roofs[k]["frac"] <= 1.0}
+    if units:
+        b = max(units, key=lambda k: units[k]["frac"])
+        names = {"vmem_return": "TD: texture-data unit (vector-memory return to VGPRs)",
+                 "valu_issue": "VALU issue", "scalar_issue": "scalar pipe (SALU + branch)"}
+        out["binding_unit"] = {"unit": b, "what": names[b], "busy_frac": units[b]["frac"],
+                               "others": {k: v["frac"] for k, v in units.items() if k != b}}
+        if b == "vmem_return":
+            out["binding_unit"]["ta_busy_frac"] = units[b]["ta_busy_frac"]
+            out["binding_unit"]["td_tc_stall_frac"] = units[b]["td_tc_stall_frac"]
+    if pmc and pmc.get("vmem_rd_insts_per_launch") and touched_bytes:
+        rd = float(pmc["vmem_rd_insts_per_launch"])
+        charged = rd * VMEM_CHARGE_BYTES
+        out["waste"] = round(charged / touched_bytes, 4)
+        out["charged_bytes"] = int(charged)
+        out["vmem_rd_insts_per_launch"] = int(rd)
+        tcp = pmc.get("tcp_cache_accesses_per_launch")
+        if tcp:
+            out["waste_l1"] = round(tcp * 64.0 / touched_bytes, 4)
+        out["waste_source"] = (src + ": SQ_INSTS_VMEM_RD x 64 lanes x 16 B (charged) and "
+                               "TCP_TOTAL_CACHE_ACCESSES x 64 B (waste_l1) over the D4 bytes")
+    out["roofs"] = roofs
     if not pmc:
         out["pmc"] = pmc_note
     return out
@@ -347,7 +390,8 @@ def main():
         slabs = [sharder.new_slab(torch, device=dev) for _ in range(F)]
         packed = slabs[0]
 
-    events = []
+    events = []     # [render start, render end] per timed frame
+    gu_events = []  # [render end, step end (gather + unpack enqueued)] per timed frame (tile path)
     recording = [False]
 
     def on_render(k, phase):
@@ -356,9 +400,13 @@ def main():
         if phase == 0:
             events.append([torch.cuda.Event(enable_timing=True), None])
             events[-1][0].record(streams[k])
-        else:
+        elif phase == 1:
             events[-1][1] = torch.cuda.Event(enable_timing=True)
             events[-1][1].record(streams[k])
+        else:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(streams[k])
+            gu_events.append([events[-1][1], e])
 
     if not tiled:
         def step(i: int, record: bool):
@@ -410,6 +458,36 @@ def main():
     elapsed = time.perf_counter() - t0
 
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else float("nan")
+    tile_report = None
+    if tiled and not args.shard:
+        # VERDICT r03 item 4, outside the timed region: per-rank render and
+        # gather+unpack spans of the timed frames, this rank's tiles rendered
+        # alone (one frame at a time), rank 0's whole frame alone
+        gu_ms = float(np.mean([a.elapsed_time(b) for a, b in gu_events])) if gu_events else 0.0
+
+        def alone(fn, n=5):
+            ts_ = []
+            for _ in range(n):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                fn()
+                e1.record(stream)
+                e1.synchronize()
+                ts_.append(e0.elapsed_time(e1))
+            return float(np.median(ts_))
+
+        if world > 1:
+            dist.barrier()
+        share_ms = alone(lambda: r.render_tiles(my_ids, ts, packed.data_ptr(), sptr))
+        if world > 1:
+            dist.barrier()
+        whole_ms = None
+        if rank == 0:
+            wbuf = torch.empty_like(frame)
+            whole_ms = alone(lambda: r.render(wbuf.data_ptr(), sptr))
+        from raytracingstudy_amd.dist import rank_timing_report
+        tile_report = rank_timing_report(kern_ms, gu_ms, share_ms, whole_ms)
     red_dev = dev if args.backend == "nccl" else torch.device("cpu")
     el_t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
     tot = cnt.clone().to(red_dev)
@@ -481,6 +559,11 @@ def main():
             torch.cuda.synchronize(dev)
             used = frames[:min(F, args.warmup + args.steps)]  # slots that received a frame
             out["config"]["tiles_frame_check"] = all(bool(torch.equal(whole, f)) for f in used)
+            if tile_report is not None:
+                if args.same_device:
+                    tile_report["note"] = ("rehearsal: every rank on one GPU, so the per-rank times "
+                                           "include the other ranks' kernels")
+                out["config"]["tile_path"] = tile_report
         if world == 1 and not args.shard and args.secondary:
             out["secondary"] = {}
             for name in [c for c in args.secondary.split(",") if c and c != cfg.name]:

@@ -83,8 +83,11 @@ enum {
                                       camera, size, scene and tile list stay unchanged; every
                                       frame adds spp samples */
     RT_FLAG_COMPAT_FMA = 1u << 6,  /* compat mode: evaluate getRay (include/camera.h:31-34) with
-                                      the FMA contraction nvcc's default -fmad=true applies to
-                                      the reference binary; off = source order */
+                                      ONE CANDIDATE of the FMA contraction nvcc's default
+                                      -fmad=true may apply to the reference binary; which order
+                                      that binary really uses is unpinned here (no nvcc).  Off
+                                      (default) = the reference's SOURCE semantics, in source
+                                      order */
     /* bits 8..9, test-only: what fills the padding after the last leaf list
      * (DESIGN.md §4): 0 zero spheres (default), 1 NaN spheres, 2 spheres
      * covering the root box.  Images and counters are the same for all three. */

@@ -75,10 +75,12 @@ __device__ __forceinline__ bool hit_root_box(const float o[3], float d0, float d
     return fmaxf(fmaxf(tx0, ty0), tz0) < fminf(fminf(tx1, ty1), tz1);
 }
 
-// getRay as the reference BINARY evaluates it: nvcc's default -fmad=true
-// contracts include/camera.h:31-34 (dz = 1 folds; the DAG combiner fuses an
-// fadd of two products through its first operand).  Same operations as
-// the oracle's contracted getRay, contract = 1.
+// getRay under ONE CANDIDATE contraction of include/camera.h:31-34 (dz = 1
+// folds; an fadd of two products fused through its first operand), a guess at
+// what nvcc's default -fmad=true does to the reference binary.  Which order
+// that binary really uses cannot be checked without nvcc: unpinned
+// (DESIGN.md 2.1).  The default (get_ray) is the SOURCE semantics.  Same
+// operations as the oracle's contracted getRay, contract = 1.
 __device__ __forceinline__ void get_ray_fma(const CamArgs& c, float u, float v, float& wx,
                                             float& wy, float& wz) {
     const float dx = (u - c.K[2]) / c.K[0];

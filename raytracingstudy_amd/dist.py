@@ -18,7 +18,7 @@ import numpy as np
 
 from . import tiles as T
 
-__all__ = ["TileSharder", "TileFramePipeline"]
+__all__ = ["TileSharder", "TileFramePipeline", "rank_timing_report"]
 
 
 class TileSharder:
@@ -124,7 +124,9 @@ class TileFramePipeline:
     current (``torch.cuda.stream``), or None on CPU.  ``gather=False``
     renders only (a local projection of one rank's share, no collective).
     ``on_render(k, phase)`` is called with phase 0 / 1 right before / after
-    the render call (bench.py records its HIP events there).
+    the render call, and with phase 2 once the step's gather and unpack are
+    enqueued (bench.py records its HIP events there: 0 -> 1 is the render,
+    1 -> 2 the gather + unpack as slot k's stream sees them).
     """
 
     def __init__(self, sharder: TileSharder, slabs, render: Callable, unpack: Callable,
@@ -164,3 +166,48 @@ class TileFramePipeline:
         if work is not None:
             work.wait()
         self.sharder.unpack_fused(gathered, lambda buf, ids: self.unpack(k, buf, ids))
+        if self.on_render is not None:
+            self.on_render(k, 2)
+
+
+def rank_timing_report(render_ms: float, gather_unpack_ms: float, share_ms: float,
+                       whole_ms: Optional[float] = None, group=None) -> Optional[dict]:
+    """Per-rank timings of the tile path, collected on rank 0 (VERDICT r03
+    item 4: the N>1 bench line explains itself).  Every rank passes
+      render_ms        its mean render span over the timed frames (HIP events
+                       on the slot stream; with frames in flight a span also
+                       covers the other slot's overlapping kernels),
+      gather_unpack_ms its mean span from render end to the step's end (the
+                       gather, plus the fused unpack on rank 0),
+      share_ms         its tiles rendered alone, one frame at a time (the clean
+                       per-rank kernel time),
+    and rank 0 the whole frame rendered alone (whole_ms).  Returns, on rank 0,
+    {ranks_seen, render_ms {min, max}, share_ms {min, max}, gather_unpack_ms
+    {rank0, max}, ideal_share_ms = whole_ms / ranks, slowest_share_over_ideal};
+    None elsewhere.  Outside any timed region (one all_gather_object)."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    mine = [float(render_ms), float(gather_unpack_ms), float(share_ms)]
+    if world > 1:
+        allv: list = [None] * world
+        dist.all_gather_object(allv, mine, group=group)
+    else:
+        allv = [mine]
+    if rank != 0:
+        return None
+    rend = [v[0] for v in allv]
+    gu = [v[1] for v in allv]
+    sh = [v[2] for v in allv]
+    out = {"ranks_seen": world,
+           "render_ms": {"min": round(min(rend), 4), "max": round(max(rend), 4)},
+           "share_ms": {"min": round(min(sh), 4), "max": round(max(sh), 4)},
+           "gather_unpack_ms": {"rank0": round(gu[0], 4), "max": round(max(gu), 4)},
+           "per_rank": [{"render_ms": round(a, 4), "gather_unpack_ms": round(b, 4),
+                         "share_ms": round(c, 4)} for a, b, c in allv]}
+    if whole_ms:
+        ideal = float(whole_ms) / world
+        out["whole_frame_ms"] = round(float(whole_ms), 4)
+        out["ideal_share_ms"] = round(ideal, 4)
+        out["slowest_share_over_ideal"] = round(max(sh) / ideal, 4)
+    return out

@@ -1,6 +1,7 @@
-"""bench.py's roofline block (CPU): every roof comes from measured data, a
-fraction above 1 is never reported, and algorithmic (cache-served) bytes are
-never priced against HBM."""
+"""bench.py's roofline block (CPU): the headline is SURVEY 8d D4's algorithmic
+bytes over the peak of the level that serves them (the L2 aggregate), the
+literal HBM pricing and the counter HBM fraction ride beside it, the busiest
+unit is named separately, and every figure comes from measured data."""
 import json
 import os
 
@@ -21,18 +22,27 @@ def _pmc(cfg="c3"):
         return json.load(f)[cfg]
 
 
-def test_valu_issue_is_the_bound_when_hbm_traffic_is_tiny():
+def test_headline_is_d4_bytes_over_the_l2_peak():
+    """frac is recomputable by one division."""
     pmc = _pmc()
     kern_ms = pmc["scene_kernel_avg_ns"] / 1e6
-    # C3 touches ~182 GB of node/sphere records per launch:
-    # more than HBM could move in that time, so it must not be an HBM fraction
-    touched = 182.19e9
+    # C3 touches ~191 GB of node/sphere records per launch (SURVEY 8d D4):
+    # more than HBM could move in that time
+    touched = 191.32e9
     r = bench.roofline(kern_ms, touched, pmc, SIMDS)
-    assert r["frac"] is not None and 0 < r["frac"] <= 1.0
+    assert r["bound"] == "l2" and r["peak"] == bench.L2_PEAK_GBS and r["unit"] == "GB/s"
+    assert r["frac"] == pytest.approx(touched / (kern_ms / 1e3) / 34.5e12, rel=1e-3)
+    assert r["achieved"] == pytest.approx(touched / (kern_ms / 1e3) / 1e9, rel=1e-3)
+    # the literal D3 pricing against HBM is reported, above 1 and marked not HBM-served
+    h = r["hbm_literal"]
+    assert h["frac"] == pytest.approx(touched / (kern_ms / 1e3) / 8e12, rel=1e-3)
+    assert h["frac"] > 1.0 and h["hbm_served"] is False
+    # the counters' HBM bytes are a tiny fraction of peak
     assert r["traffic"] / touched < 0.01
-    # an issue roof (scalar pipe or VALU) or the vector-memory return path
-    # binds, never HBM
-    assert r["bound"] in ("scalar_issue", "valu_issue", "vmem_return")
+    assert r["hbm_counter"]["frac"] == pytest.approx(r["traffic"] / (kern_ms / 1e3) / 8e12, rel=1e-3)
+    # the busiest unit is reported separately, never as the roofline
+    assert r["binding_unit"]["unit"] in ("scalar_issue", "valu_issue", "vmem_return")
+    assert 0 < r["binding_unit"]["busy_frac"] <= 1.0
     v = r["roofs"]["valu_issue"]
     insts = pmc["sq"]["SQ_INSTS_VALU"]
     peak = SIMDS * pmc["effective_clock_ghz"] / 2.0  # G wave-instructions / s
@@ -48,19 +58,32 @@ def test_vmem_return_roof_from_td_busy():
     assert v["peak"] == pytest.approx(SIMDS / 4 * pmc["effective_clock_ghz"], rel=1e-3)
     assert v["achieved"] == pytest.approx(0.9 * v["peak"], rel=1e-3)
     assert v["ta_busy_frac"] == pytest.approx(0.8) and v["td_tc_stall_frac"] == pytest.approx(0.1)
-    valid = {k: x["frac"] for k, x in r["roofs"].items() if x["frac"] <= 1.0}
-    assert r["bound"] == max(valid, key=valid.get)
+    units = {k: r["roofs"][k]["frac"] for k in ("vmem_return", "valu_issue", "scalar_issue")
+             if k in r["roofs"] and r["roofs"][k]["frac"] <= 1.0}
+    assert r["binding_unit"]["unit"] == max(units, key=units.get)
     # a summary without the TA/TD pass has no such roof
     q = {k: x for k, x in _pmc().items() if k not in ("td_busy_frac", "ta_busy_frac", "td_tc_stall_frac")}
     assert "vmem_return" not in bench.roofline(q["scene_kernel_avg_ns"] / 1e6, 1e9, q, SIMDS)["roofs"]
 
 
-def test_over_unity_roofs_are_never_chosen():
+def test_over_unity_units_are_never_named_binding():
     pmc = dict(_pmc())
     pmc["sq"] = dict(pmc["sq"], SQ_INSTS_VALU=pmc["sq"]["SQ_INSTS_VALU"] * 5)  # impossible rate
     r = bench.roofline(pmc["scene_kernel_avg_ns"] / 1e6, 1e9, pmc, SIMDS)
     assert r["roofs"]["valu_issue"]["frac"] > 1.0
-    assert r["bound"] != "valu_issue" and (r["frac"] is None or r["frac"] <= 1.0)
+    assert r["binding_unit"]["unit"] != "valu_issue" and r["bound"] == "l2"
+
+
+def test_waste_is_charged_over_algorithmic_bytes():
+    """the vector-memory instructions per launch (profile
+    pass 6) priced at 64 lanes x 16 B, over the D4 bytes."""
+    pmc = dict(_pmc(), vmem_rd_insts_per_launch=272e6, tcp_cache_accesses_per_launch=4.19e9)
+    r = bench.roofline(pmc["scene_kernel_avg_ns"] / 1e6, 191.32e9, pmc, SIMDS)
+    assert r["charged_bytes"] == int(272e6 * 1024)
+    assert r["waste"] == pytest.approx(272e6 * 1024 / 191.32e9, rel=1e-3)
+    assert r["waste_l1"] == pytest.approx(4.19e9 * 64 / 191.32e9, rel=1e-3)
+    q = {k: v for k, v in _pmc().items() if k != "vmem_rd_insts_per_launch"}
+    assert "waste" not in bench.roofline(8.6, 191e9, q, SIMDS)
 
 
 def test_without_pmc_only_the_cache_roof_remains():
@@ -107,6 +130,7 @@ def test_scalar_issue_roof_when_counted():
     s = r["roofs"]["scalar_issue"]
     peak = SIMDS / 4 * pmc["effective_clock_ghz"]  # G instr/s
     assert s["frac"] == pytest.approx((4.81 + 1.13) / (kern_ms / 1e3) / peak, rel=1e-3)
-    # the binding roof is the largest valid fraction
-    valid = {k: v["frac"] for k, v in r["roofs"].items() if v["frac"] <= 1}
-    assert r["bound"] == max(valid, key=valid.get)
+    # the binding unit is the busiest valid one
+    units = {k: r["roofs"][k]["frac"] for k in ("vmem_return", "valu_issue", "scalar_issue")
+             if k in r["roofs"] and r["roofs"][k]["frac"] <= 1}
+    assert r["binding_unit"]["unit"] == max(units, key=units.get)

@@ -143,7 +143,8 @@ def test_committed_pmc_summary_feeds_the_bench_roofline():
     ent, why = bench.load_pmc(path, "c3", 1, kernel_source_id(), rt.CONFIGS["c3"].leaf_capacity)
     assert ent is not None, why
     r = bench.roofline(ent["scene_kernel_avg_ns"] / 1e6, 182e9, ent, 1024)
-    assert r["bound"] in ("scalar_issue", "valu_issue", "vmem_return") and 0.0 < r["frac"] <= 1.0
+    assert r["bound"] == "l2" and 0.0 < r["frac"] <= 1.0
+    assert r["binding_unit"]["unit"] in ("scalar_issue", "valu_issue", "vmem_return")
     assert "scalar_issue" in r["roofs"] and "valu_issue" in r["roofs"]
     assert r["traffic"] and r["traffic"] > 0
     assert bench.load_pmc(path, "c4", 1, kernel_source_id())[0] is None  # not profiled

@@ -105,12 +105,30 @@ def _rank_main(rank, world, port, w, h, spp, q):
     def unpack(k, buf, ids):
         T.unpack_host(buf.numpy().reshape(-1, 64, 64, 4), ids, w, h, out=frames[k])
 
-    pipe = TileFramePipeline(sh, slabs, render, unpack)
+    phases = []
+    pipe = TileFramePipeline(sh, slabs, render, unpack, on_render=lambda k, ph: phases.append((k, ph)))
     works = []
     for i in range(3):
         pipe.step(i)
         works.append(pipe.last_work)
     assert rendered == [0, 1, 0]
+    # bench.py's event hooks: before / after the render, and after gather + unpack
+    assert phases == [(0, 0), (0, 1), (0, 2), (1, 0), (1, 1), (1, 2), (0, 0), (0, 1), (0, 2)]
+    # the per-rank timings bench.py adds to an N>1 line
+    from raytracingstudy_amd.dist import rank_timing_report
+    rep = rank_timing_report(1.0 + rank, 0.25 * (rank + 1), 1.1 + 0.1 * rank,
+                             whole_ms=8.0 if rank == 0 else None)
+    if rank == 0:
+        assert rep["ranks_seen"] == world
+        assert rep["render_ms"] == {"min": 1.0, "max": 1.0 + (world - 1)}
+        assert rep["gather_unpack_ms"]["rank0"] == 0.25
+        assert rep["gather_unpack_ms"]["max"] == 0.25 * world
+        assert rep["share_ms"]["max"] == round(1.1 + 0.1 * (world - 1), 4)
+        assert rep["ideal_share_ms"] == round(8.0 / world, 4)
+        assert rep["slowest_share_over_ideal"] == round((1.1 + 0.1 * (world - 1)) / (8.0 / world), 4)
+        assert len(rep["per_rank"]) == world
+    else:
+        assert rep is None
     assert all(wk is not None and hasattr(wk, "wait") for wk in works)
     if rank == 0:
         recv = sh.__dict__["_recv_bufs"]

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise a tools/ab_libs2.sh log: per (config, library) the per-process
+"""Summarise a tools/ab_libs.sh log: per (config, library) the per-process
 kernel medians and their median, plus each library's change against the first.
 
     python tools/ab_summary.py gpurun_out/r03/mt_ab.log
@@ -14,6 +14,8 @@ def main(path):
     runs = collections.defaultdict(list)
     libs = []
     for line in open(path):
+        if line.startswith("#") or not line.strip():
+            continue  # the "# cmd: ..." header of tools/ab_libs.sh
         lib, cfg, js = line.split(" ", 2)
         if lib not in libs:
             libs.append(lib)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Wave-execution counts of the walk's blocks (diagnostic build).
 
-    bash tools/build_flags.sh bstats -DRT_BLOCK_STATS
+    bash tools/build_exp.sh bstats -DRT_BLOCK_STATS
     RT_AMD_LIB=abl/librt_bstats.so python tools/block_stats.py --configs c3,c5
 
 One stats frame per config; the library appends, per frame, how many times a

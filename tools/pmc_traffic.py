@@ -122,6 +122,19 @@ def main():
         res["td_busy_frac"] = vm["TD_TD_BUSY_sum"][0] / cu_cycles
         res["ta_busy_frac"] = vm.get("TA_TA_BUSY_sum", (0, 0))[0] / cu_cycles
         res["td_tc_stall_frac"] = vm.get("TD_TC_STALL_sum", (0, 0))[0] / cu_cycles
+    vi = counters(os.path.join(root, "vinst"))
+    if vi.get("SQ_INSTS_VMEM_RD"):
+        # vector-memory wave-instructions and L1 (TCP) cache accesses per
+        # launch (profile pass 6): bench.py prices each read instruction at
+        # 64 lanes x 16 B (the TD's per-instruction charge)
+        res["vinst"] = {k: v[0] for k, v in vi.items()}
+        res["vmem_rd_insts_per_launch"] = vi["SQ_INSTS_VMEM_RD"][0]
+        res["vmem_wr_insts_per_launch"] = vi.get("SQ_INSTS_VMEM_WR", (0, 0))[0]
+        res["ta_flat_read_wavefronts_per_launch"] = vi.get("TA_FLAT_READ_WAVEFRONTS_sum", (0, 0))[0]
+        res["tcp_cache_accesses_per_launch"] = vi.get("TCP_TOTAL_CACHE_ACCESSES_sum", (0, 0))[0]
+    cmd = os.path.join(root, "command.txt")
+    if os.path.exists(cmd):
+        res["command"] = open(cmd).read().strip()
     print(json.dumps(res, indent=1))
 
 

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-wave timeline of the wave-queue scene kernel (diagnostic build).
 
-    bash tools/build_flags.sh timeline -DRT_TIMELINE
+    bash tools/build_exp.sh timeline -DRT_TIMELINE
     RT_AMD_LIB=abl/librt_timeline.so python tools/timeline.py [--config c3] [--n 8]
 
 Renders the full frame and rank 0's N-way share a few times; every frame's
