@@ -30,6 +30,8 @@
  *   cudaGraphicsResourceGetMappedPointer + unmap          rt_render(dev_rgba8 = mapped ptr)
  *     src/renderer.cu:145-151
  *   (none: single device)                                 rt_render_tiles / rt_unpack_tiles
+ *   (none: single device; SURVEY 8b B2 "device ids",      rt_create_multi / rt_get_multi_info
+ *     8e E1 ncclCommInitAll)
  *   (none: no error reporting, all void)                  rt_last_error
  *
  * Threading: one handle per host thread / stream; calls on one handle are not
@@ -46,7 +48,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 typedef struct rt_renderer rt_renderer;
 
@@ -281,6 +283,48 @@ void* rt_framebuffer(rt_renderer* r);
  * default stream (src/renderer.cu:149).  Renderers made one after another get
  * streams on different hardware queues, so frames in flight on them overlap. */
 void* rt_stream(rt_renderer* r);
+
+/* ---- one process, several devices (SURVEY 8b B2 "device ids", 8e E1) ------ */
+/* A renderer handle that renders every frame across n_devices GPUs of this
+ * process: one renderer per device (same config, same scene: replicated), the
+ * frame's 64x64 tiles dealt round-robin (tile t to device t mod n), each
+ * device rendering its tiles into a packed slab on its own stream, the slabs
+ * moved to devices[0] (RCCL: one ncclCommInitAll communicator over the
+ * devices, grouped ncclSend / ncclRecv on per-device comm streams; or peer
+ * copies) and unpacked there by ONE launch into the frame.  Two frames are in
+ * flight: frame k+1's tiles render while frame k's slabs travel and unpack.
+ * Every other entry point works on the handle as on a single-device one
+ * (rt_set_pose / rt_set_intrinsic / rt_resize / rt_set_scene / rt_set_octree
+ * / rt_reset_accumulation apply to every device; rt_set_scene_device takes a
+ * sphere list on devices[0] and broadcasts it (ncclBroadcast); rt_render,
+ * rt_bind_graphics_resource / rt_bind_display, rt_readback, rt_framebuffer,
+ * rt_stream, rt_get_scene_info and rt_export_octree are devices[0]'s), except
+ * rt_render_tiles / rt_unpack_tiles (RT_E_STATE: the handle renders whole
+ * frames).  rt_render with stats renders the devices one after another and
+ * sums their counters (ms = host wall time of the frame).  The reference's
+ * Displayer (src/window/displayer.cpp:28) constructs the renderer this way
+ * and calls render() unchanged.
+ * devices: HIP ordinals; a repeated ordinal (e.g. {0,0,0,0}) rehearses the
+ * n-way plan on fewer GPUs (peer-copy transport only: RCCL refuses a device
+ * twice in one communicator).  cfg->device is ignored. */
+enum {
+    RT_TRANSPORT_AUTO = 0, /* RCCL when the devices are distinct and librccl loads, else peer */
+    RT_TRANSPORT_RCCL = 1, /* grouped ncclSend / ncclRecv over one ncclCommInitAll communicator */
+    RT_TRANSPORT_PEER = 2  /* hipMemcpyPeerAsync on the comm streams (xGMI, or a local copy) */
+};
+#define RT_MAX_DEVICES 16
+typedef struct rt_multi_info {
+    uint32_t n_devices;              /* 1 for a single-device handle                     */
+    int32_t devices[RT_MAX_DEVICES]; /* HIP ordinals, devices[0] holds the frame           */
+    uint32_t transport;              /* RT_TRANSPORT_RCCL or RT_TRANSPORT_PEER (0: single)  */
+    uint32_t tile_size;              /* 64                                                */
+    uint32_t slab_tiles;             /* tiles per device slab (ceil(tiles / n_devices))   */
+    uint32_t frames_in_flight;       /* 2                                                 */
+    uint64_t frames;                 /* frames rendered by the handle                     */
+} rt_multi_info;
+int rt_create_multi(const rt_config* cfg, const int32_t* devices, uint32_t n_devices,
+                    uint32_t transport, rt_renderer** out);
+int rt_get_multi_info(const rt_renderer* r, rt_multi_info* info);
 
 /* ---- errors --------------------------------------------------------------- */
 /* Last error message for this handle (r may be NULL: last global error). */

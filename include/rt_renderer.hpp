@@ -57,6 +57,20 @@ public:
         setGraphicsResource(graphics_resource);
     }
     explicit KernelRenderer(const rt_config& cfg) { check(rt_create(&cfg, &r_)); }
+    // One process, several GPUs (rt_create_multi): every render()
+    // draws the frame across `devices` (tiles round-robin, slabs to devices[0]
+    // over RCCL or peer copies, one unpack); every other method is unchanged.
+    // The Displayer (src/window/displayer.cpp:28) only swaps this constructor in.
+    KernelRenderer(const rt_config& cfg, const std::vector<int>& devices,
+                   uint32_t transport = RT_TRANSPORT_AUTO) {
+        check(rt_create_multi(&cfg, devices.data(), static_cast<uint32_t>(devices.size()), transport,
+                              &r_));
+    }
+    rt_multi_info multiInfo() const {
+        rt_multi_info i;
+        check(rt_get_multi_info(r_, &i), r_);
+        return i;
+    }
     ~KernelRenderer() { rt_destroy(r_); }
     KernelRenderer(const KernelRenderer&) = delete;
     KernelRenderer& operator=(const KernelRenderer&) = delete;

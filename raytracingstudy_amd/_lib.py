@@ -43,6 +43,11 @@ RT_CELL_TABLE_OFF = 15
 VARIANT_REMOVED = 2  # a removed variant number (the packet walk): rt_create refuses it
 VARIANT_BLOCK = 7   # unified walk, block-tile queue (default for spp < 8)
 VARIANT_WAVEQ = 13  # unified walk, per-wave per-XCD queues (default for spp >= 8)
+VARIANT_WAVEQ_LOW = 4  # the same queue for spp < 8 (default for spp < 8 since round 4)
+RT_TRANSPORT_AUTO = 0
+RT_TRANSPORT_RCCL = 1
+RT_TRANSPORT_PEER = 2
+RT_MAX_DEVICES = 16
 
 _f3 = ctypes.c_float * 3
 
@@ -118,6 +123,25 @@ DISPLAY_MAP = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
 DISPLAY_UNMAP = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)
 
 
+class RtMultiInfo(ctypes.Structure):
+    _fields_ = [
+        ("n_devices", ctypes.c_uint32),
+        ("devices", ctypes.c_int32 * 16),
+        ("transport", ctypes.c_uint32),
+        ("tile_size", ctypes.c_uint32),
+        ("slab_tiles", ctypes.c_uint32),
+        ("frames_in_flight", ctypes.c_uint32),
+        ("frames", ctypes.c_uint64),
+    ]
+
+    def as_dict(self) -> dict:
+        n = int(self.n_devices)
+        return {"n_devices": n, "devices": [int(self.devices[i]) for i in range(n)],
+                "transport": {0: "single", 1: "rccl", 2: "peer"}.get(int(self.transport), "?"),
+                "tile_size": int(self.tile_size), "slab_tiles": int(self.slab_tiles),
+                "frames_in_flight": int(self.frames_in_flight), "frames": int(self.frames)}
+
+
 class RtDisplayOps(ctypes.Structure):
     _fields_ = [("map", DISPLAY_MAP), ("unmap", DISPLAY_UNMAP)]
 
@@ -158,6 +182,9 @@ SIGNATURES = {
     "rt_framebuffer": (_P, [_P]),
     "rt_stream": (_P, [_P]),
     "rt_last_error": (ctypes.c_char_p, [_P]),
+    "rt_create_multi": (_int, [ctypes.POINTER(RtConfig), ctypes.POINTER(ctypes.c_int32), _u32, _u32,
+                               ctypes.POINTER(_P)]),
+    "rt_get_multi_info": (_int, [_P, ctypes.POINTER(RtMultiInfo)]),
 }
 
 _lock = threading.Lock()

@@ -5,14 +5,17 @@
 // the kernels by value; device buffers are owned here (the reference leaks
 // its device-heap Camera/Octree, src/renderer.cu:189-198); every call returns
 // a status (the reference's render path checks nothing, :145-151).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <rccl/rccl.h>  // types only: the functions are resolved at run time (rccl_api)
 #include <stdio.h>
 #include <string.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -32,6 +35,32 @@ hipError_t launch_unpack(const uint32_t* packed, const uint32_t* tiles, uint32_t
 }  // namespace rtamd
 
 using namespace rtamd;
+
+// rt_create_multi: the frame's tiles over several
+// devices of this process; `r` (the handle) is devices[0]'s renderer
+struct MultiState {
+    static constexpr int F = 2;            // frames in flight
+    static constexpr uint32_t kTs = 64;    // tile side
+    std::vector<int> devs;                 // devs[0] = the handle's device
+    std::vector<rt_renderer*> peers;       // peers[k] renders device k's tiles (peers[0] = the handle)
+    uint32_t transport = 0;                // RT_TRANSPORT_RCCL / RT_TRANSPORT_PEER
+    std::vector<ncclComm_t> comms;         // one per device (ncclCommInitAll)
+    std::vector<hipStream_t> cs;           // per-device comm stream
+    // per frame slot f: each device's packed slab, devices[0]'s receive buffer
+    // of n slabs end to end, and the events that order their reuse
+    std::vector<void*> slab[F];
+    void* recv[F] = {nullptr, nullptr};
+    std::vector<hipEvent_t> rendered[F], sent[F];
+    hipEvent_t recvd[F] = {nullptr, nullptr}, unpacked[F] = {nullptr, nullptr}, out_ready = nullptr;
+    bool used[F] = {false, false};
+    uint64_t frame = 0;
+    // tile plan for the current size
+    uint32_t W = 0, H = 0, S = 0;          // S = slab tiles
+    size_t slab_bytes = 0;
+    std::vector<std::vector<uint32_t>> ids;
+    std::vector<uint32_t> all_ids;         // n * S, padding slots RT_TILE_SKIP
+    uint32_t* d_all_ids = nullptr;         // on devices[0]
+};
 
 namespace {
 thread_local std::string g_last_error;
@@ -104,9 +133,31 @@ struct rt_renderer {
     SceneArgs sc{};
     rt_scene_info info{};
     std::string err;
+    // multi-device handle (rt_create_multi): this renderer is devices[0]'s
+    // part; the state holds the other devices' renderers and the transport
+    MultiState* multi = nullptr;
 };
 
 namespace {
+
+// multi-device handle internals (defined with rt_create_multi below)
+int multi_render(rt_renderer* r, uint32_t* out, hipStream_t hs, rt_stats* stats);
+int multi_synchronize(rt_renderer* r);
+void multi_destroy(rt_renderer* r);
+int multi_set_scene_device(rt_renderer* r, uint32_t n, const rt_octree_params* oct);
+// apply `fn` to every other device's renderer of a multi-device handle
+template <typename Fn>
+int for_peers(rt_renderer* r, Fn fn) {
+    if (!r || !r->multi) return RT_OK;
+    for (size_t k = 1; k < r->multi->peers.size(); ++k) {
+        const int st = fn(r->multi->peers[k]);
+        if (st) {
+            r->err = r->multi->peers[k]->err + " (device " + std::to_string(r->multi->devs[k]) + ")";
+            return st;
+        }
+    }
+    return RT_OK;
+}
 
 int fail(rt_renderer* r, int code, const std::string& msg) {
     g_last_error = msg;
@@ -138,6 +189,11 @@ int ensure(rt_renderer* r, DevBuf<T>& b, size_t n) {
     b.n = n;
     return RT_OK;
 }
+
+int render_tiles_one(rt_renderer* r, const uint32_t* tile_ids, uint32_t n_tiles, uint32_t ts,
+                     void* dev_packed, void* stream, rt_stats* stats);
+int unpack_tiles_one(rt_renderer* r, const void* dev_packed, const uint32_t* tile_ids,
+                     uint32_t n_tiles, uint32_t ts, void* dev_rgba8, void* stream);
 
 int set_device(rt_renderer* r) {
     RT_HIP(r, hipSetDevice(r->device));
@@ -190,7 +246,10 @@ void fill_frame_args(rt_renderer* r, FrameArgs& a) {
     // spp < 8: the block-tile queue with counters only in stats frames (C2
     // 0.185 -> 0.168 ms against the always-counting build 7,
     // profiles/r02/c2_variant_ab.log)
-    a.variant = v ? v : (a.spp >= 8u ? kVariantWaveQ : kVariantLaneUnified2NoStats);
+    // round 4: spp < 8 frames take the per-wave queue too (variant 4, no
+    // workgroup barrier per block tile: C2 0.155 -> 0.107 ms,
+    // profiles/r04/c2_waveq_ab.log)
+    a.variant = v ? v : (a.spp >= 8u ? kVariantWaveQ : kVariantWaveQLow);
 }
 
 // Build the octree of the device sphere list (d_spheres) and point the
@@ -608,7 +667,7 @@ int rt_create(const rt_config* cfg, rt_renderer** out) {
         return fail(nullptr, RT_E_INVALID, "rt_create: unknown mode");
     if (!variant_available((cfg->flags >> RT_FLAG_VARIANT_SHIFT) & 0xFu))
         return fail(nullptr, RT_E_INVALID,
-                    "rt_create: scene-kernel variant not in this build (0, 7, 10 or 13)");
+                    "rt_create: scene-kernel variant not in this build (0, 4, 7, 10 or 13)");
     if (((cfg->flags >> (RT_FLAG_OPT_SHIFT + kOptChunkShift)) & 7u) > kOptChunkMax)
         return fail(nullptr, RT_E_INVALID,
                     "rt_create: wave-queue ticket size field (flags bits 24..26) must be 0..4");
@@ -665,6 +724,7 @@ int rt_create(const rt_config* cfg, rt_renderer** out) {
 
 int rt_destroy(rt_renderer* r) {
     if (!r) return RT_OK;
+    if (r->multi) multi_destroy(r);
     (void)hipSetDevice(r->device);
     if (r->stream) (void)hipStreamSynchronize(r->stream);
     if (r->pending) (void)hipEventSynchronize(r->done);  // work on a caller's stream
@@ -692,14 +752,14 @@ int rt_set_pose(rt_renderer* r, const float pose[16]) {
     if (!r || !pose) return fail(r, RT_E_INVALID, "rt_set_pose: null argument");
     if (memcmp(r->pose, pose, sizeof(r->pose)) != 0) r->frames_accum = 0;
     memcpy(r->pose, pose, sizeof(r->pose));
-    return RT_OK;
+    return for_peers(r, [&](rt_renderer* p) { return rt_set_pose(p, pose); });
 }
 
 int rt_set_intrinsic(rt_renderer* r, const float K[9]) {
     if (!r || !K) return fail(r, RT_E_INVALID, "rt_set_intrinsic: null argument");
     if (memcmp(r->K, K, sizeof(r->K)) != 0) r->frames_accum = 0;
     memcpy(r->K, K, sizeof(r->K));
-    return RT_OK;
+    return for_peers(r, [&](rt_renderer* p) { return rt_set_intrinsic(p, K); });
 }
 
 int rt_get_camera(const rt_renderer* r, float pose_out[16], float K_out[9]) {
@@ -725,7 +785,8 @@ int rt_resize(rt_renderer* r, uint32_t width, uint32_t height) {
     if (r->cfg.flags & RT_FLAG_RADIANCE)
         if ((st = ensure(r, r->rad, (size_t)width * height))) return st;
     rt_resize_intrinsic(width, height, r->K);
-    return RT_OK;
+    if (r->multi && (st = multi_synchronize(r))) return st;  // the slabs are re-planned
+    return for_peers(r, [&](rt_renderer* p) { return rt_resize(p, width, height); });
 }
 
 int rt_set_scene(rt_renderer* r, const float* spheres, const uint32_t* albedo, uint32_t n,
@@ -758,7 +819,8 @@ int rt_set_scene(rt_renderer* r, const float* spheres, const uint32_t* albedo, u
     }
     r->info.upload_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return build_scene(r);
+    if ((st = build_scene(r))) return st;
+    return for_peers(r, [&](rt_renderer* p) { return rt_set_scene(p, spheres, albedo, n, oct); });
 }
 
 int rt_set_scene_device(rt_renderer* r, const void* dev_spheres, const void* dev_albedo,
@@ -799,7 +861,10 @@ int rt_set_scene_device(rt_renderer* r, const void* dev_spheres, const void* dev
     r->host_copy = false;
     r->info.upload_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return build_scene(r);
+    if ((st = build_scene(r))) return st;
+    // a multi-device handle: the validated list (now in d_spheres / d_albedo
+    // on devices[0]) is broadcast to the other devices, which build their trees
+    return r->multi ? multi_set_scene_device(r, n, oct) : RT_OK;
 }
 
 int rt_set_octree(rt_renderer* r, const float mn[3], const float mx[3], float resolution) {
@@ -814,8 +879,9 @@ int rt_set_octree(rt_renderer* r, const float mn[3], const float mx[3], float re
     p.resolution = resolution;
     p.max_depth = 0;
     r->oct = p;
-    if (!r->has_scene) return RT_OK;
-    return build_scene(r);
+    int st;
+    if (r->has_scene && (st = build_scene(r))) return st;
+    return for_peers(r, [&](rt_renderer* q) { return rt_set_octree(q, mn, mx, resolution); });
 }
 
 int rt_get_scene_info(const rt_renderer* r, rt_scene_info* info) {
@@ -869,12 +935,18 @@ int rt_render(rt_renderer* r, void* dev_rgba8, void* stream, rt_stats* stats) {
     if (!r) return fail(r, RT_E_INVALID, "rt_render: null handle");
     int st;
     if ((st = set_device(r))) return st;
-    accum_pixels(r, nullptr, 0, 0);
+    // (a multi-device handle's renderers accumulate per tile list, in multi_render)
+    if (!r->multi) accum_pixels(r, nullptr, 0, 0);
     FrameArgs a;
     fill_frame_args(r, a);
     a.out8 = dev_rgba8 ? static_cast<uint32_t*>(dev_rgba8) : r->fb.p;
     a.out32 = (r->cfg.flags & RT_FLAG_RADIANCE) ? r->rad.p : nullptr;
-    if (dev_rgba8 || !r->disp.map) return do_render(r, a, stream, stats);
+    if (r->multi && (r->cfg.flags & RT_FLAG_RADIANCE))
+        return fail(r, RT_E_STATE, "rt_render: a multi-device handle keeps no radiance buffer");
+    const auto render_into = [&](hipStream_t hs) -> int {
+        return r->multi ? multi_render(r, a.out8, hs, stats) : do_render(r, a, hs, stats);
+    };
+    if (dev_rgba8 || !r->disp.map) return render_into(static_cast<hipStream_t>(stream));
     // the reference's render(): map the PBO, launch into it, unmap
     // (src/renderer.cu:145-151)
     hipStream_t hs = stream ? static_cast<hipStream_t>(stream) : r->stream;
@@ -892,7 +964,7 @@ int rt_render(rt_renderer* r, void* dev_rgba8, void* stream, rt_stats* stats) {
         return fail(r, RT_E_INVALID, "rt_render: display buffer smaller than W*H*4 bytes");
     }
     a.out8 = static_cast<uint32_t*>(ptr);
-    st = do_render(r, a, hs, stats);
+    st = render_into(hs);
     const int eu = r->disp.unmap(r->disp_user, hs);
     if (st) return st;
     if (eu != 0) {
@@ -942,6 +1014,24 @@ int rt_bind_graphics_resource(rt_renderer* r, void* resource) {
 int rt_render_tiles(rt_renderer* r, const uint32_t* tile_ids, uint32_t n_tiles, uint32_t ts,
                     void* dev_packed, void* stream, rt_stats* stats) {
     if (!r) return fail(r, RT_E_INVALID, "rt_render_tiles: null handle");
+    if (r->multi)
+        return fail(r, RT_E_STATE, "rt_render_tiles: a multi-device handle renders whole frames");
+    return render_tiles_one(r, tile_ids, n_tiles, ts, dev_packed, stream, stats);
+}
+
+int rt_unpack_tiles(rt_renderer* r, const void* dev_packed, const uint32_t* tile_ids,
+                    uint32_t n_tiles, uint32_t ts, void* dev_rgba8, void* stream) {
+    if (!r) return fail(r, RT_E_INVALID, "rt_unpack_tiles: null handle");
+    if (r->multi)
+        return fail(r, RT_E_STATE, "rt_unpack_tiles: a multi-device handle renders whole frames");
+    return unpack_tiles_one(r, dev_packed, tile_ids, n_tiles, ts, dev_rgba8, stream);
+}
+
+}  // extern "C"
+
+namespace {
+int render_tiles_one(rt_renderer* r, const uint32_t* tile_ids, uint32_t n_tiles, uint32_t ts,
+                     void* dev_packed, void* stream, rt_stats* stats) {
     if (n_tiles && (!tile_ids || !dev_packed))
         return fail(r, RT_E_INVALID, "rt_render_tiles: null argument");
     int st;
@@ -978,9 +1068,8 @@ int rt_render_tiles(rt_renderer* r, const uint32_t* tile_ids, uint32_t n_tiles, 
     return st;
 }
 
-int rt_unpack_tiles(rt_renderer* r, const void* dev_packed, const uint32_t* tile_ids,
-                    uint32_t n_tiles, uint32_t ts, void* dev_rgba8, void* stream) {
-    if (!r) return fail(r, RT_E_INVALID, "rt_unpack_tiles: null handle");
+int unpack_tiles_one(rt_renderer* r, const void* dev_packed, const uint32_t* tile_ids,
+                     uint32_t n_tiles, uint32_t ts, void* dev_rgba8, void* stream) {
     if (n_tiles && (!tile_ids || !dev_packed)) return fail(r, RT_E_INVALID, "rt_unpack_tiles: null argument");
     int st;
     if ((st = check_tiles(r, tile_ids, n_tiles, ts, /*allow_skip=*/true))) return st;
@@ -996,11 +1085,14 @@ int rt_unpack_tiles(rt_renderer* r, const void* dev_packed, const uint32_t* tile
     if (e != hipSuccess) return hip_fail(r, e, "rt_unpack_tiles");
     return mark_queued(r, s);
 }
+}  // namespace
+
+extern "C" {
 
 int rt_reset_accumulation(rt_renderer* r) {
     if (!r) return fail(r, RT_E_INVALID, "rt_reset_accumulation: null handle");
     r->frames_accum = 0;
-    return RT_OK;
+    return for_peers(r, [](rt_renderer* p) { return rt_reset_accumulation(p); });
 }
 
 // After the renderer's work has completed: the wave queue's bounded wait
@@ -1020,6 +1112,7 @@ static int check_last_frame(rt_renderer* r) {
 int rt_synchronize(rt_renderer* r) {
     if (!r) return RT_E_INVALID;
     int st;
+    if (r->multi && (st = multi_synchronize(r))) return st;
     if ((st = set_device(r))) return st;
     RT_HIP(r, hipStreamSynchronize(r->stream));
     if (r->pending) RT_HIP(r, hipEventSynchronize(r->done));
@@ -1029,6 +1122,7 @@ int rt_synchronize(rt_renderer* r) {
 int rt_readback(rt_renderer* r, uint8_t* host_rgba8, float* host_rgba32f) {
     if (!r) return RT_E_INVALID;
     int st;
+    if (r->multi && (st = multi_synchronize(r))) return st;
     if ((st = set_device(r))) return st;
     // the frame may have been queued on a caller's stream
     RT_HIP(r, hipStreamSynchronize(r->stream));
@@ -1051,6 +1145,437 @@ void* rt_stream(rt_renderer* r) { return r ? static_cast<void*>(r->stream) : nul
 const char* rt_last_error(const rt_renderer* r) {
     if (r) return r->err.c_str();
     return g_last_error.c_str();
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Multi-device handle (rt_create_multi; SURVEY 8b B2 "device ids", 8e E1)
+//
+// One process drives n devices.  Frame j uses slot f = j mod 2:
+//   device k, its renderer's stream : [wait sent[f][k]]  render its tiles -> slab[f][k]
+//                                      record rendered[f][k]
+//   device k, comm stream cs[k]     : wait rendered[f][k]; send slab[f][k] to device 0
+//                                      record sent[f][k]
+//   device 0, comm stream cs[0]     : [wait unpacked[f]]; receive slab k into
+//                                      recv[f] + k * slab; record recvd[f]
+//   device 0, output stream hs      : record out_ready; cs[0] waits it and recvd[f], unpacks
+//                                      the n slabs in ONE launch into the frame; hs waits
+//                                      unpacked[f]
+// so frame j+1's tiles render while frame j's slabs travel and unpack, and a
+// slab or receive buffer is rewritten only after its previous frame let go of
+// it.  Transport: RCCL (grouped ncclSend / ncclRecv over one ncclCommInitAll
+// communicator, device 0 receiving from itself too) or peer copies
+// (hipMemcpyPeerAsync: distinct devices over xGMI, or the same device in a
+// rehearsal of the n-way plan on one GPU).
+// ---------------------------------------------------------------------------
+namespace {
+
+// RCCL resolved at run time: librt_amd.so does not link it, so a process that
+// already holds one (torch's) shares it, and single-device use never loads it.
+struct RcclApi {
+    bool ok = false;
+    std::string why;
+    ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t,
+                              hipStream_t) = nullptr;
+    const char* (*ErrorString)(ncclResult_t) = nullptr;
+};
+
+RcclApi& rccl_api() {
+    static RcclApi api;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            api.why = std::string("librccl.so.1 not loadable: ") + dlerror();
+            return;
+        }
+        bool all = true;
+        auto sym = [&](const char* n) {
+            void* p = dlsym(h, n);
+            if (!p) all = false;
+            return p;
+        };
+        api.CommInitAll = reinterpret_cast<decltype(api.CommInitAll)>(sym("ncclCommInitAll"));
+        api.CommDestroy = reinterpret_cast<decltype(api.CommDestroy)>(sym("ncclCommDestroy"));
+        api.GroupStart = reinterpret_cast<decltype(api.GroupStart)>(sym("ncclGroupStart"));
+        api.GroupEnd = reinterpret_cast<decltype(api.GroupEnd)>(sym("ncclGroupEnd"));
+        api.Send = reinterpret_cast<decltype(api.Send)>(sym("ncclSend"));
+        api.Recv = reinterpret_cast<decltype(api.Recv)>(sym("ncclRecv"));
+        api.Broadcast = reinterpret_cast<decltype(api.Broadcast)>(sym("ncclBroadcast"));
+        api.ErrorString = reinterpret_cast<decltype(api.ErrorString)>(sym("ncclGetErrorString"));
+        api.ok = all;
+        if (!all) api.why = "librccl.so.1 lacks a required symbol";
+    });
+    return api;
+}
+
+int nccl_fail(rt_renderer* r, ncclResult_t e, const char* what) {
+    const char* m = rccl_api().ErrorString ? rccl_api().ErrorString(e) : "?";
+    return fail(r, RT_E_HIP, std::string(what) + ": RCCL error " + std::to_string((int)e) + " (" + m + ")");
+}
+
+#define RT_NCCL(r, call)                                         \
+    do {                                                         \
+        ncclResult_t e_ = (call);                                \
+        if (e_ != ncclSuccess) return nccl_fail((r), e_, #call); \
+    } while (0)
+
+// (Re)plan the tiles and the buffers for the handle's current size: tile t to
+// device t mod n (interleaved, so a centred scene balances), slabs
+// of S = ceil(T / n) tiles, the gathered slabs unpacked with padding slots
+// skipped.  Waits for in-flight frames before it frees anything.
+int multi_plan(rt_renderer* r) {
+    MultiState& m = *r->multi;
+    if (m.W == r->W && m.H == r->H && m.recv[0]) return RT_OK;
+    int st;
+    if ((st = multi_synchronize(r))) return st;
+    const uint32_t n = static_cast<uint32_t>(m.devs.size()), ts = MultiState::kTs;
+    const uint32_t T = ((r->W + ts - 1) / ts) * ((r->H + ts - 1) / ts);
+    m.S = (T + n - 1) / n;
+    m.slab_bytes = (size_t)m.S * ts * ts * 4;
+    m.ids.assign(n, {});
+    for (uint32_t t = 0; t < T; ++t) m.ids[t % n].push_back(t);
+    m.all_ids.assign((size_t)n * m.S, RT_TILE_SKIP);
+    for (uint32_t k = 0; k < n; ++k)
+        std::copy(m.ids[k].begin(), m.ids[k].end(), m.all_ids.begin() + (size_t)k * m.S);
+    for (int f = 0; f < MultiState::F; ++f) {
+        for (uint32_t k = 0; k < n; ++k) {
+            RT_HIP(r, hipSetDevice(m.devs[k]));
+            if (m.slab[f][k]) (void)hipFree(m.slab[f][k]);
+            m.slab[f][k] = nullptr;
+            RT_HIP(r, hipMalloc(&m.slab[f][k], m.slab_bytes));
+        }
+        RT_HIP(r, hipSetDevice(m.devs[0]));
+        if (m.recv[f]) (void)hipFree(m.recv[f]);
+        m.recv[f] = nullptr;
+        RT_HIP(r, hipMalloc(&m.recv[f], m.slab_bytes * n));
+        m.used[f] = false;
+    }
+    RT_HIP(r, hipSetDevice(m.devs[0]));
+    if (m.d_all_ids) (void)hipFree(m.d_all_ids);
+    m.d_all_ids = nullptr;
+    RT_HIP(r, hipMalloc(reinterpret_cast<void**>(&m.d_all_ids), m.all_ids.size() * sizeof(uint32_t)));
+    RT_HIP(r, hipMemcpy(m.d_all_ids, m.all_ids.data(), m.all_ids.size() * sizeof(uint32_t),
+                        hipMemcpyHostToDevice));
+    m.W = r->W;
+    m.H = r->H;
+    return RT_OK;
+}
+
+int multi_synchronize(rt_renderer* r) {
+    MultiState& m = *r->multi;
+    for (size_t k = 0; k < m.devs.size(); ++k) {
+        RT_HIP(r, hipSetDevice(m.devs[k]));
+        if (m.cs[k]) RT_HIP(r, hipStreamSynchronize(m.cs[k]));
+        rt_renderer* p = m.peers[k];
+        RT_HIP(r, hipStreamSynchronize(p->stream));
+        if (p->pending) RT_HIP(r, hipEventSynchronize(p->done));
+    }
+    for (int f = 0; f < MultiState::F; ++f)
+        if (m.unpacked[f]) RT_HIP(r, hipEventSynchronize(m.unpacked[f]));
+    return RT_OK;
+}
+
+int multi_render(rt_renderer* r, uint32_t* out, hipStream_t hs, rt_stats* stats) {
+    MultiState& m = *r->multi;
+    int st;
+    if (r->cfg.mode == RT_MODE_SCENE && !r->has_scene)
+        return fail(r, RT_E_NOSCENE, "RT_MODE_SCENE render without rt_set_scene");
+    if ((st = multi_plan(r))) return st;
+    if (!hs) hs = r->stream;
+    const uint32_t n = static_cast<uint32_t>(m.devs.size()), ts = MultiState::kTs;
+    const int f = static_cast<int>(m.frame % MultiState::F);
+    const auto t0 = std::chrono::steady_clock::now();
+    rt_stats sum{};
+    // 1. every device renders its tiles into its slab of slot f
+    for (uint32_t k = 0; k < n; ++k) {
+        rt_renderer* p = m.peers[k];
+        RT_HIP(r, hipSetDevice(m.devs[k]));
+        if (m.used[f]) RT_HIP(r, hipStreamWaitEvent(p->stream, m.sent[f][k], 0));
+        rt_stats sk{};
+        st = render_tiles_one(p, m.ids[k].data(), static_cast<uint32_t>(m.ids[k].size()), ts,
+                              m.slab[f][k], p->stream, stats ? &sk : nullptr);
+        if (st) {
+            r->err = p->err + " (device " + std::to_string(m.devs[k]) + ")";
+            return st;
+        }
+        if (stats) {
+            sum.primary_rays += sk.primary_rays;
+            sum.shadow_rays += sk.shadow_rays;
+            sum.nodes_visited += sk.nodes_visited;
+            sum.prims_tested += sk.prims_tested;
+            sum.samples_per_pixel = sk.samples_per_pixel;
+        }
+        RT_HIP(r, hipEventRecord(m.rendered[f][k], p->stream));
+        RT_HIP(r, hipStreamWaitEvent(m.cs[k], m.rendered[f][k], 0));
+    }
+    // 2. the slabs to devices[0]: recv[f] + k * slab
+    RT_HIP(r, hipSetDevice(m.devs[0]));
+    if (m.used[f]) RT_HIP(r, hipStreamWaitEvent(m.cs[0], m.unpacked[f], 0));
+    char* rb = static_cast<char*>(m.recv[f]);
+    if (m.transport == RT_TRANSPORT_RCCL) {
+        RcclApi& api = rccl_api();
+        RT_NCCL(r, api.GroupStart());
+        for (uint32_t k = 0; k < n; ++k) {
+            ncclResult_t e = api.Send(m.slab[f][k], m.slab_bytes, ncclUint8, 0, m.comms[k], m.cs[k]);
+            if (e == ncclSuccess)
+                e = api.Recv(rb + k * m.slab_bytes, m.slab_bytes, ncclUint8, static_cast<int>(k),
+                             m.comms[0], m.cs[0]);
+            if (e != ncclSuccess) {
+                (void)api.GroupEnd();
+                return nccl_fail(r, e, "ncclSend/ncclRecv");
+            }
+        }
+        RT_NCCL(r, api.GroupEnd());
+        for (uint32_t k = 0; k < n; ++k) {
+            RT_HIP(r, hipSetDevice(m.devs[k]));
+            RT_HIP(r, hipEventRecord(m.sent[f][k], m.cs[k]));
+        }
+    } else {
+        for (uint32_t k = 0; k < n; ++k) {
+            RT_HIP(r, hipSetDevice(m.devs[k]));
+            // the copy writes devices[0]'s receive buffer from device k's stream:
+            // after frame j-2's unpack has read it
+            if (k && m.used[f]) RT_HIP(r, hipStreamWaitEvent(m.cs[k], m.unpacked[f], 0));
+            RT_HIP(r, hipMemcpyPeerAsync(rb + k * m.slab_bytes, m.devs[0], m.slab[f][k], m.devs[k],
+                                         m.slab_bytes, m.cs[k]));
+            RT_HIP(r, hipEventRecord(m.sent[f][k], m.cs[k]));
+        }
+        RT_HIP(r, hipSetDevice(m.devs[0]));
+        for (uint32_t k = 1; k < n; ++k) RT_HIP(r, hipStreamWaitEvent(m.cs[0], m.sent[f][k], 0));
+    }
+    // 3. one unpack of all slabs on devices[0], after the output stream's
+    //    earlier work (a mapped display buffer is ready) and the slabs' arrival
+    RT_HIP(r, hipSetDevice(m.devs[0]));
+    RT_HIP(r, hipEventRecord(m.recvd[f], m.cs[0]));
+    RT_HIP(r, hipEventRecord(m.out_ready, hs));
+    RT_HIP(r, hipStreamWaitEvent(m.cs[0], m.out_ready, 0));
+    hipError_t e = launch_unpack(static_cast<const uint32_t*>(m.recv[f]), m.d_all_ids, n * m.S, ts,
+                                 (r->W + ts - 1) / ts, r->W, r->H, out, m.cs[0]);
+    if (e != hipSuccess) return hip_fail(r, e, "multi-device unpack");
+    RT_HIP(r, hipEventRecord(m.unpacked[f], m.cs[0]));
+    RT_HIP(r, hipStreamWaitEvent(hs, m.unpacked[f], 0));
+    m.used[f] = true;
+    ++m.frame;
+    if (stats) {
+        RT_HIP(r, hipStreamSynchronize(hs));
+        sum.ms = static_cast<float>(
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        if (r->cfg.mode != RT_MODE_SCENE) sum.primary_rays = (uint64_t)r->W * r->H;
+        *stats = sum;
+    }
+    return RT_OK;
+}
+
+int multi_set_scene_device(rt_renderer* r, uint32_t n, const rt_octree_params* oct) {
+    MultiState& m = *r->multi;
+    const uint32_t nd = static_cast<uint32_t>(m.devs.size());
+    if (nd < 2) return RT_OK;
+    // each other device receives the list into a scratch pair, then builds
+    std::vector<void*> sp(nd, nullptr), al(nd, nullptr);
+    int st = RT_OK;
+    auto release = [&] {
+        for (uint32_t k = 1; k < nd; ++k) {
+            (void)hipSetDevice(m.devs[k]);
+            if (sp[k]) (void)hipFree(sp[k]);
+            if (al[k]) (void)hipFree(al[k]);
+        }
+        (void)hipSetDevice(m.devs[0]);
+    };
+    const size_t nb = std::max<size_t>(1, (size_t)n) * sizeof(float4);
+    const size_t ab = std::max<size_t>(1, (size_t)n) * sizeof(uint32_t);
+    for (uint32_t k = 1; k < nd && !st; ++k) {
+        hipError_t e = hipSetDevice(m.devs[k]);
+        if (e == hipSuccess) e = hipMalloc(&sp[k], nb);
+        if (e == hipSuccess) e = hipMalloc(&al[k], ab);
+        if (e != hipSuccess) st = hip_fail(r, e, "rt_set_scene_device: broadcast buffers");
+    }
+    if (!st && n) {
+        if (m.transport == RT_TRANSPORT_RCCL) {
+            // ncclBroadcast from devices[0]: spheres as 4n floats, albedo as n words
+            RcclApi& api = rccl_api();
+            ncclResult_t e = api.GroupStart();
+            for (uint32_t k = 0; k < nd && e == ncclSuccess; ++k) {
+                void* dst = k ? sp[k] : r->d_spheres.p;
+                e = api.Broadcast(r->d_spheres.p, dst, (size_t)n * 4, ncclFloat32, 0, m.comms[k], m.cs[k]);
+                if (e == ncclSuccess)
+                    e = api.Broadcast(r->d_albedo.p, k ? al[k] : r->d_albedo.p, n, ncclUint32, 0,
+                                      m.comms[k], m.cs[k]);
+            }
+            const ncclResult_t e2 = api.GroupEnd();
+            if (e == ncclSuccess) e = e2;
+            if (e != ncclSuccess) st = nccl_fail(r, e, "ncclBroadcast");
+        } else {
+            for (uint32_t k = 1; k < nd && !st; ++k) {
+                hipError_t e = hipSetDevice(m.devs[k]);
+                if (e == hipSuccess)
+                    e = hipMemcpyPeerAsync(sp[k], m.devs[k], r->d_spheres.p, m.devs[0], nb, m.cs[k]);
+                if (e == hipSuccess)
+                    e = hipMemcpyPeerAsync(al[k], m.devs[k], r->d_albedo.p, m.devs[0], ab, m.cs[k]);
+                if (e != hipSuccess) st = hip_fail(r, e, "rt_set_scene_device: peer copy");
+            }
+        }
+    }
+    for (uint32_t k = 1; k < nd && !st; ++k) {
+        st = rt_set_scene_device(m.peers[k], sp[k], al[k], n, oct, m.cs[k]);
+        if (st) r->err = m.peers[k]->err + " (device " + std::to_string(m.devs[k]) + ")";
+    }
+    release();
+    return st;
+}
+
+void multi_destroy(rt_renderer* r) {
+    MultiState* m = r->multi;
+    (void)multi_synchronize(r);
+    r->multi = nullptr;
+    const size_t n = m->devs.size();
+    for (size_t k = 0; k < n; ++k) {
+        (void)hipSetDevice(m->devs[k]);
+        for (int f = 0; f < MultiState::F; ++f) {
+            if (k < m->slab[f].size() && m->slab[f][k]) (void)hipFree(m->slab[f][k]);
+            if (k < m->rendered[f].size() && m->rendered[f][k]) (void)hipEventDestroy(m->rendered[f][k]);
+            if (k < m->sent[f].size() && m->sent[f][k]) (void)hipEventDestroy(m->sent[f][k]);
+        }
+        if (k < m->comms.size() && m->comms[k]) (void)rccl_api().CommDestroy(m->comms[k]);
+        if (k < m->cs.size() && m->cs[k]) (void)hipStreamDestroy(m->cs[k]);
+        if (k && m->peers[k]) rt_destroy(m->peers[k]);
+    }
+    (void)hipSetDevice(m->devs[0]);
+    for (int f = 0; f < MultiState::F; ++f) {
+        if (m->recv[f]) (void)hipFree(m->recv[f]);
+        if (m->recvd[f]) (void)hipEventDestroy(m->recvd[f]);
+        if (m->unpacked[f]) (void)hipEventDestroy(m->unpacked[f]);
+    }
+    if (m->out_ready) (void)hipEventDestroy(m->out_ready);
+    if (m->d_all_ids) (void)hipFree(m->d_all_ids);
+    delete m;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_create_multi(const rt_config* cfg, const int32_t* devices, uint32_t n_devices,
+                    uint32_t transport, rt_renderer** out) {
+    if (!cfg || !devices || !out) return fail(nullptr, RT_E_INVALID, "rt_create_multi: null argument");
+    *out = nullptr;
+    if (n_devices == 0 || n_devices > RT_MAX_DEVICES)
+        return fail(nullptr, RT_E_INVALID, "rt_create_multi: n_devices must be 1..16");
+    if (transport > RT_TRANSPORT_PEER) return fail(nullptr, RT_E_INVALID, "rt_create_multi: unknown transport");
+    const int ndev = rt_device_count();
+    bool distinct = true;
+    for (uint32_t i = 0; i < n_devices; ++i) {
+        if (devices[i] < 0 || devices[i] >= ndev)
+            return fail(nullptr, RT_E_INVALID, "rt_create_multi: device ordinal out of range");
+        for (uint32_t j = 0; j < i; ++j)
+            if (devices[j] == devices[i]) distinct = false;
+    }
+    if (transport == RT_TRANSPORT_RCCL && !distinct)
+        return fail(nullptr, RT_E_INVALID,
+                    "rt_create_multi: RCCL needs distinct devices (a repeated ordinal is a "
+                    "peer-copy rehearsal)");
+    if (transport == RT_TRANSPORT_AUTO) transport = distinct && rccl_api().ok ? RT_TRANSPORT_RCCL : RT_TRANSPORT_PEER;
+    if (transport == RT_TRANSPORT_RCCL && !rccl_api().ok)
+        return fail(nullptr, RT_E_INVALID, "rt_create_multi: " + rccl_api().why);
+    rt_config c0 = *cfg;
+    c0.device = devices[0];
+    rt_renderer* r = nullptr;
+    int st = rt_create(&c0, &r);
+    if (st) return st;
+    MultiState* m = new (std::nothrow) MultiState();
+    if (!m) {
+        rt_destroy(r);
+        return fail(nullptr, RT_E_NOMEM, "rt_create_multi: out of host memory");
+    }
+    r->multi = m;
+    m->transport = transport;
+    m->devs.assign(devices, devices + n_devices);
+    m->peers.assign(n_devices, nullptr);
+    m->peers[0] = r;
+    m->cs.assign(n_devices, nullptr);
+    for (int f = 0; f < MultiState::F; ++f) {
+        m->slab[f].assign(n_devices, nullptr);
+        m->rendered[f].assign(n_devices, nullptr);
+        m->sent[f].assign(n_devices, nullptr);
+    }
+    auto bail = [&](int code) {
+        g_last_error = r->err.empty() ? g_last_error : r->err;
+        rt_destroy(r);  // frees the multi state and the peers made so far
+        return code;
+    };
+    for (uint32_t k = 1; k < n_devices; ++k) {
+        rt_config ck = *cfg;
+        ck.device = devices[k];
+        if ((st = rt_create(&ck, &m->peers[k]))) {
+            r->err = g_last_error;
+            return bail(st);
+        }
+    }
+    for (uint32_t k = 0; k < n_devices; ++k) {
+        hipError_t e = hipSetDevice(devices[k]);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&m->cs[k], hipStreamNonBlocking);
+        for (int f = 0; f < MultiState::F && e == hipSuccess; ++f) {
+            e = hipEventCreateWithFlags(&m->rendered[f][k], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&m->sent[f][k], hipEventDisableTiming);
+        }
+        if (e != hipSuccess) return bail(hip_fail(r, e, "rt_create_multi: streams/events"));
+        if (k && transport == RT_TRANSPORT_PEER && devices[k] != devices[0]) {
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, devices[0], devices[k]) == hipSuccess && can) {
+                (void)hipSetDevice(devices[0]);
+                (void)hipDeviceEnablePeerAccess(devices[k], 0);  // already enabled is fine
+                (void)hipGetLastError();
+            }
+        }
+    }
+    {
+        hipError_t e = hipSetDevice(devices[0]);
+        for (int f = 0; f < MultiState::F && e == hipSuccess; ++f) {
+            e = hipEventCreateWithFlags(&m->recvd[f], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&m->unpacked[f], hipEventDisableTiming);
+        }
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&m->out_ready, hipEventDisableTiming);
+        if (e != hipSuccess) return bail(hip_fail(r, e, "rt_create_multi: events"));
+    }
+    if (transport == RT_TRANSPORT_RCCL) {
+        m->comms.assign(n_devices, nullptr);
+        const ncclResult_t e = rccl_api().CommInitAll(m->comms.data(), static_cast<int>(n_devices), devices);
+        if (e != ncclSuccess) {
+            m->comms.clear();
+            return bail(nccl_fail(r, e, "ncclCommInitAll"));
+        }
+    }
+    (void)hipSetDevice(devices[0]);
+    *out = r;
+    return RT_OK;
+}
+
+int rt_get_multi_info(const rt_renderer* r, rt_multi_info* info) {
+    if (!r || !info) return RT_E_INVALID;
+    memset(info, 0, sizeof(*info));
+    info->tile_size = MultiState::kTs;
+    if (!r->multi) {
+        info->n_devices = 1;
+        info->devices[0] = r->device;
+        return RT_OK;
+    }
+    const MultiState& m = *r->multi;
+    info->n_devices = static_cast<uint32_t>(m.devs.size());
+    for (size_t k = 0; k < m.devs.size(); ++k) info->devices[k] = m.devs[k];
+    info->transport = m.transport;
+    const uint32_t ts = MultiState::kTs, n = info->n_devices;
+    info->slab_tiles = (((r->W + ts - 1) / ts) * ((r->H + ts - 1) / ts) + n - 1) / n;
+    info->frames_in_flight = MultiState::F;
+    info->frames = m.frame;
+    return RT_OK;
 }
 
 }  // extern "C"

@@ -15,11 +15,12 @@
 // moves the camera through the Displayer's controller (W held every frame);
 // --progressive accumulates samples while the camera stays put.
 //
-// --gpus N: one process drives N devices: renderer k renders
-// the 64x64 tiles t = k, k+N, ... into a packed slab on device k; the slabs
-// are copied peer-to-peer (xGMI) to device 0 and unpacked there into the
-// frame.  --same-device puts all N renderers on device 0 (a logic rehearsal
-// on one GPU).
+// --gpus N: one process drives N devices through the C-ABI's
+// multi-device handle (rt_create_multi): device k renders the 64x64 tiles
+// t = k, k+N, ... into a packed slab, the slabs go to device 0 over RCCL and
+// are unpacked there into the frame, two frames in flight.  --same-device puts
+// all N renderers on device 0 (a rehearsal of the plan on one GPU; peer-copy
+// transport, since RCCL refuses a device twice).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -28,20 +29,9 @@
 #include <string>
 #include <vector>
 
-#include <hip/hip_runtime.h>
-
-#include <memory>
 
 #include "../../include/rt_camera.hpp"
 #include "../../include/rt_renderer.hpp"
-
-namespace {
-
-void hip_check(hipError_t e, const char* what) {
-    if (e != hipSuccess) throw rtamd::Error(RT_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
-}
-
-}  // namespace
 
 int write_ppm(const std::string& out, const std::vector<uint8_t>& img, int W, int H) {
     FILE* f = fopen(out.c_str(), "wb");
@@ -55,15 +45,17 @@ int write_ppm(const std::string& out, const std::vector<uint8_t>& img, int W, in
     return 0;
 }
 
-// One process, N devices: renderer 0 (already set up) plus N-1 more with the
-// same scene; tiles interleaved over renderers; peer copies to device 0.
-int run_multi(rtamd::KernelRenderer& r0, const rt_config& rc, const float pose[16], int gpus,
-              bool same_device, int frames, const std::string& out, int W, int H, int spp,
-              int depth, long n, const std::string& scene_in) {
+// One process, N devices: the C-ABI's multi-device handle
+// (rt_create_multi) renders every frame across the devices: tiles
+// round-robin, each device's slab to device 0 over RCCL (grouped ncclSend /
+// ncclRecv on per-device comm streams; peer copies for a --same-device
+// rehearsal), one unpack, two frames in flight.
+int run_multi(const rt_config& rc, const float pose[16], int gpus, bool same_device, int frames,
+              const std::string& out, int W, int H, int spp, int depth, long n,
+              const std::string& scene_in) {
     const int ndev = rt_device_count();
     if (ndev < 1) throw rtamd::Error(RT_E_HIP, "no HIP device");
     if (!same_device && ndev < gpus) throw rtamd::Error(RT_E_INVALID, "fewer devices than --gpus");
-    const uint32_t ts = 64, tx = (W + ts - 1) / ts, ty = (H + ts - 1) / ts, T = tx * ty;
     std::vector<float> sp;
     std::vector<uint32_t> al;
     if (!scene_in.empty()) {
@@ -76,82 +68,39 @@ int run_multi(rtamd::KernelRenderer& r0, const rt_config& rc, const float pose[1
     rt_octree_params p;
     rt_octree_params_default(&p);
     p.max_depth = (uint32_t)depth;
-    std::vector<std::unique_ptr<rtamd::KernelRenderer>> more;
-    std::vector<rtamd::KernelRenderer*> rs{&r0};
-    std::vector<int> dev{0};  // renderer 0 runs on the current device (0)
-    for (int k = 1; k < gpus; ++k) {
-        rt_config c = rc;
-        c.device = same_device ? 0 : k;
-        more.emplace_back(new rtamd::KernelRenderer(c));
-        more.back()->resize(W, H);
-        more.back()->setPosition(pose);
-        more.back()->setScene(sp, al, &p);
-        rs.push_back(more.back().get());
-        dev.push_back(c.device);
+    std::vector<int> devs(gpus);
+    for (int k = 0; k < gpus; ++k) devs[k] = same_device ? 0 : k;
+    rtamd::KernelRenderer r(rc, devs);
+    r.resize(W, H);
+    r.setPosition(pose);
+    r.setScene(sp, al, &p);
+    const rt_multi_info mi = r.multiInfo();
+    rt_stats st{};
+    r.render(nullptr, nullptr, &st);  // counted frame (devices one after another)
+    const uint64_t rays = st.primary_rays + st.shadow_rays;
+    r.synchronize();
+    // timed: frames back to back, two in flight, one wait at the end
+    const int timed = frames > 0 ? frames : 1;
+    auto t0 = std::chrono::steady_clock::now();
+    for (int f = 0; f < timed; ++f) {
+        r.setPosition(pose);  // the Displayer sets the pose every frame
+        r.render();
     }
-    std::vector<std::vector<uint32_t>> ids(gpus);
-    for (uint32_t t = 0; t < T; ++t) ids[t % gpus].push_back(t);
-    const size_t slab_bytes = ids[0].size() * ts * ts * 4;
-    std::vector<void*> slab(gpus, nullptr), on0(gpus, nullptr);
-    for (int k = 0; k < gpus; ++k) {
-        hip_check(hipSetDevice(dev[k]), "hipSetDevice");
-        hip_check(hipMalloc(&slab[k], slab_bytes), "hipMalloc slab");
-        if (k && dev[k] != dev[0]) {
-            hip_check(hipSetDevice(dev[0]), "hipSetDevice");
-            hip_check(hipMalloc(&on0[k], slab_bytes), "hipMalloc gather");
-            int can = 0;
-            hip_check(hipDeviceCanAccessPeer(&can, dev[0], dev[k]), "hipDeviceCanAccessPeer");
-            if (can) (void)hipDeviceEnablePeerAccess(dev[k], 0);
-        } else {
-            on0[k] = slab[k];
-        }
-    }
-    double best = 1e30, best_kernel = 0;
-    uint64_t rays = 0;
-    for (int f = 0; f < frames; ++f) {
-        for (auto* r : rs) r->setPosition(pose);
-        auto t0 = std::chrono::steady_clock::now();
-        std::vector<rt_stats> st(gpus);
-        for (int k = 0; k < gpus; ++k) rs[k]->renderTiles(ids[k], ts, slab[k], nullptr, nullptr);
-        for (int k = 0; k < gpus; ++k) rs[k]->synchronize();
-        for (int k = 1; k < gpus; ++k)
-            if (on0[k] != slab[k])
-                hip_check(hipMemcpyPeer(on0[k], dev[0], slab[k], dev[k], ids[k].size() * ts * ts * 4),
-                          "hipMemcpyPeer");
-        for (int k = 0; k < gpus; ++k) rs[0]->unpackTiles(on0[k], ids[k], ts);
-        rs[0]->synchronize();
-        auto t1 = std::chrono::steady_clock::now();
-        best = std::min(best, std::chrono::duration<double, std::milli>(t1 - t0).count());
-        if (f == frames - 1) {  // a counted frame: per-renderer kernel time and rays
-            double mx = 0;
-            rays = 0;
-            for (int k = 0; k < gpus; ++k) {
-                rs[k]->renderTiles(ids[k], ts, slab[k], nullptr, &st[k]);
-                mx = std::max(mx, (double)st[k].ms);
-                rays += st[k].primary_rays + st[k].shadow_rays;
-            }
-            best_kernel = mx;
-        }
-    }
-    printf("%d renderers on %s: %dx%d spp %d: frame %.3f ms (tiles + peer gather + unpack), "
-           "slowest renderer kernel %.3f ms, %llu rays, %.1f Mrays/s\n",
-           gpus, same_device ? "device 0" : "devices 0..N-1", W, H, spp, best, best_kernel,
-           (unsigned long long)rays, rays / (best * 1e3));
-    int rc_out = 0;
+    r.synchronize();
+    const double ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / timed;
+    printf("%d devices (%s, transport %s): %dx%d spp %d: %.3f ms/frame over %d frames "
+           "(tiles + %s gather + unpack, 2 in flight), %llu rays, %.1f Mrays/s\n",
+           gpus, same_device ? "all on device 0" : "devices 0..N-1",
+           mi.transport == RT_TRANSPORT_RCCL ? "rccl" : "peer", W, H, spp, ms, timed,
+           mi.transport == RT_TRANSPORT_RCCL ? "RCCL" : "peer-copy", (unsigned long long)rays,
+           rays / (ms * 1e3));
     if (!out.empty()) {
         std::vector<uint8_t> img((size_t)W * H * 4);
-        rs[0]->readback(img.data());
-        rc_out = write_ppm(out, img, W, H);
+        r.readback(img.data());
+        return write_ppm(out, img, W, H);
     }
-    for (int k = 0; k < gpus; ++k) {
-        (void)hipSetDevice(dev[k]);
-        (void)hipFree(slab[k]);
-        if (on0[k] != slab[k]) {
-            (void)hipSetDevice(dev[0]);
-            (void)hipFree(on0[k]);
-        }
-    }
-    return rc_out;
+    return 0;
 }
 
 int main(int argc, char** argv) {
@@ -159,6 +108,7 @@ int main(int argc, char** argv) {
     bool host_build = false, same_device = false, progressive = false, panel = false,
          walk = false;
     int gpus = 1;
+    bool multi = false;  // --gpus given (even 1: a 1-device RCCL communicator)
     int W = 0, H = 0, spp = 0, frames = 3;
     long n = -1;
     int depth = 0;
@@ -181,7 +131,7 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--scene")) scene_in = next("--scene");
         else if (!strcmp(argv[i], "--save-scene")) scene_out = next("--save-scene");
         else if (!strcmp(argv[i], "--host-build")) host_build = true;
-        else if (!strcmp(argv[i], "--gpus")) gpus = atoi(next("--gpus"));
+        else if (!strcmp(argv[i], "--gpus")) gpus = atoi(next("--gpus")), multi = true;
         else if (!strcmp(argv[i], "--same-device")) same_device = true;
         else if (!strcmp(argv[i], "--progressive")) progressive = true;
         else if (!strcmp(argv[i], "--panel")) panel = true;
@@ -245,9 +195,10 @@ int main(int argc, char** argv) {
                    si.n_spheres, si.n_nodes, si.n_leaves, si.n_prim_refs, si.depth_reached,
                    si.max_depth, si.builder == RT_BUILDER_HOST ? "host" : "device", si.build_ms);
         }
-        if (gpus > 1) {
+        if (multi) {
+            if (gpus < 1 || gpus > RT_MAX_DEVICES) throw rtamd::Error(RT_E_INVALID, "--gpus must be 1..16");
             if (!scene) throw rtamd::Error(RT_E_INVALID, "--gpus needs a scene config");
-            return run_multi(r, rc, pose, gpus, same_device, frames, out, W, H, spp, depth, n,
+            return run_multi(rc, pose, gpus, same_device, frames, out, W, H, spp, depth, n,
                              scene_in);
         }
         rt_stats st{};

@@ -1218,9 +1218,25 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
             }
             for (uint32_t wt = wave; wt < wtiles; wt += kBlockThreads / 64) {
                 const uint32_t wox = (wt % wtx) * tw, woy = (wt / wtx) * th;
+#ifdef RT_TIMELINE
+                const unsigned long long tu0 = wall_clock64();
+#endif
                 shade_wave_tile<kTiles, kChunk, kStats, kProg>(
                     a, acc, stk, ox + wox, oy + woy, obase, n_primary, n_shadow, n_nodes,
                     n_prims, bs);
+#ifdef RT_TIMELINE
+                // per wave tile of a block tile: {start, end, hw_id << 32 | xcc << 16 |
+                // wave index}, unit id = block tile * 16 + wave tile (tools/timeline.py)
+                const unsigned long long uid = (unsigned long long)bt * 16u + wt;
+                if (a.timeline && (threadIdx.x & 63u) == 0 && uid < (1ull << 22)) {
+                    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+                    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // XCC_ID
+                    a.timeline[4ull * 65536 + 3 * uid] = tu0;
+                    a.timeline[4ull * 65536 + 3 * uid + 1] = wall_clock64();
+                    a.timeline[4ull * 65536 + 3 * uid + 2] =
+                        ((unsigned long long)hw << 32) | (xcc << 16) | (blockIdx.x * 4u + wave);
+                }
+#endif
             }
         }
     }
@@ -1470,6 +1486,19 @@ static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStr
             else
                 launch_persistent(scene_kernel<kTiles, 1, 2, false>, a, n_bt, lds, st);
             break;
+        case kVariantWaveQLow:  // the spp < 8 default (round 4): the per-wave queue, 8 waves/SIMD
+            // No workgroup barrier per block tile: the timeline of the block-tile
+            // queue (variant 10) showed waves idle 28% of the C2 launch, mostly
+            // waiting at that barrier for the slowest of a tile's 4 wave tiles
+            // (gaps p90 5.2 us against units of p50 5.8 us,
+            // profiles/r04/c2_timeline.log).  With it C2 0.155 -> 0.107 ms; the
+            // 3-workgroups-per-CU cap of the block-tile queue costs it again
+            // here (0.152 ms), so it has none (profiles/r04/c2_waveq_ab.log).
+            if (a.count_work)
+                launch_waveq(scene_kernel<kTiles, 7, 2, true, false, true>, a, lds, st);
+            else
+                launch_waveq(scene_kernel_w8<kTiles>, a, lds, st, 8);
+            break;
         case kVariantWaveQ:  // the spp >= 8 default: per-wave scheduling over per-XCD queues.
             // Timed (plain) frames: 8 waves/SIMD with SGPRs capped at 80
             // (kSceneSgprs); stats frames keep 7 (their counters need the
@@ -1490,7 +1519,7 @@ static void launch_scene_t(const FrameArgs& a, uint32_t n_bt, size_t lds, hipStr
 // removed in round 3; their A/B logs stay under profiles/.
 bool variant_available(uint32_t v) {
     return v == 0 || v == kVariantLaneUnified || v == kVariantLaneUnified2NoStats ||
-           v == kVariantWaveQ;
+           v == kVariantWaveQ || v == kVariantWaveQLow;
 }
 
 hipError_t launch_scene(const FrameArgs& a_in, hipStream_t st) {

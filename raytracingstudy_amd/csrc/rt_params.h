@@ -21,6 +21,9 @@ constexpr uint32_t kVariantLaneUnified = 7;   // one walk instance for primary +
 constexpr uint32_t kVariantLaneUnified2NoStats = 10; // spp < 8 default: 7 with counters only in stats frames
 constexpr uint32_t kVariantWaveQ = 13;     // unified walk scheduled per wave over per-XCD queues
                                            // (default for spp >= 8)
+constexpr uint32_t kVariantWaveQLow = 4;   // the per-wave queue for spp < 8 too (no workgroup
+                                           // barrier per block tile; the spp < 8 default
+                                           // since round 4)
 // prim_sp padding after the last leaf list: the leaf loads run kChunk - 1 = 1
 // sphere past a leaf's end (rt_capi.cpp fills it)
 constexpr uint32_t kPrimPad = 4;

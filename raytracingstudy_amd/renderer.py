@@ -107,7 +107,12 @@ class KernelRenderer:
                  light_dir: Sequence[float] = (1.0, 1.0, -1.0), ambient: float = 0.1,
                  variant: int = 0, opt_off: int = 0, host_build: bool = False,
                  progressive: bool = False, cell_table: Optional[int] = None,
-                 compat_fma: bool = False, pad_fill: int = 0):
+                 compat_fma: bool = False, pad_fill: int = 0,
+                 devices: Optional[Sequence[int]] = None, transport: str = "auto"):
+        """devices: render every frame across these HIP devices of this process
+        (rt_create_multi: tiles round-robin, slabs gathered to devices[0] over
+        RCCL or peer copies, one unpack); a repeated ordinal rehearses the plan
+        on fewer GPUs.  transport: "auto", "rccl" or "peer"."""
         lib = _lib.load()
         cfg = RtConfig()
         lib.rt_config_default(ctypes.byref(cfg))
@@ -152,7 +157,13 @@ class KernelRenderer:
         self.mode = mode
         self.radiance = radiance
         h = ctypes.c_void_p()
-        check(lib.rt_create(ctypes.byref(cfg), ctypes.byref(h)))
+        if devices is None:
+            check(lib.rt_create(ctypes.byref(cfg), ctypes.byref(h)))
+        else:
+            tr = {"auto": _lib.RT_TRANSPORT_AUTO, "rccl": _lib.RT_TRANSPORT_RCCL,
+                  "peer": _lib.RT_TRANSPORT_PEER}[transport]
+            devs = (ctypes.c_int32 * len(devices))(*[int(d) for d in devices])
+            check(lib.rt_create_multi(ctypes.byref(cfg), devs, len(devices), tr, ctypes.byref(h)))
         self._h = h
         self.width, self.height = int(width), int(height)
 
@@ -265,6 +276,13 @@ class KernelRenderer:
     def scene_info(self) -> dict:
         info = RtSceneInfo()
         check(self._lib.rt_get_scene_info(self._h, ctypes.byref(info)), self._h)
+        return info.as_dict()
+
+    def multi_info(self) -> dict:
+        """rt_get_multi_info: the devices, transport and tile plan of the handle
+        (n_devices 1 for a single-device renderer)."""
+        info = _lib.RtMultiInfo()
+        check(self._lib.rt_get_multi_info(self._h, ctypes.byref(info)), self._h)
         return info.as_dict()
 
     def camera(self):

@@ -129,7 +129,7 @@ def _scene_pair(oracle, n, w, h, spp, depth=7, pose=None, shadows=True, jitter=N
 # shadow walk on the block-tile queue (spp < 8 default); 10 the same with
 # counters only in stats frames; 13 per-wave per-XCD queues (spp >= 8 default).
 # The measured-and-rejected variants of DESIGN.md 5.1 were removed in round 3.
-VARIANTS = [0, 7, 10, 13]
+VARIANTS = [0, 4, 7, 10, 13]
 
 
 def _check_counts(st, cnt, variant):

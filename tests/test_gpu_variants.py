@@ -1,4 +1,4 @@
-"""Every shipped scene-kernel variant (0, 7, 10, 13) renders the oracle's
+"""Every shipped scene-kernel variant (0, 4, 7, 10, 13) renders the oracle's
 images and counters whatever the padding after the last leaf list holds.
 
 The leaf loads read one sphere past a leaf's end, which for the last leaf is

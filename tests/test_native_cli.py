@@ -59,20 +59,22 @@ def test_cli_scene_file_roundtrip_and_builders(gpu, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gpus", [2, 3])
-def test_cli_multi_renderer_frame_equals_single(gpu, tmp_path, gpus):
-    """rt_cli --gpus N (one process, N renderers, peer gather to device 0),
-    rehearsed with all renderers on device 0: the assembled frame equals the
-    single-renderer frame byte for byte."""
+@pytest.mark.parametrize("gpus,same", [(2, True), (3, True), (1, False)])
+def test_cli_multi_renderer_frame_equals_single(gpu, tmp_path, gpus, same):
+    """rt_cli --gpus N: one process, the C-ABI's multi-device handle
+    (rt_create_multi), rehearsed with all renderers on device 0
+    (peer-copy transport), and as a 1-device RCCL communicator: the assembled
+    frame equals the single-renderer frame byte for byte."""
     base = [CLI, "--config", "c3", "--spheres", "20000", "--width", "200", "--height", "150",
             "--spp", "8", "--frames", "2"]
     one, many = tmp_path / "one.ppm", tmp_path / "many.ppm"
     r1 = subprocess.run(base + ["--out", str(one)], capture_output=True, text=True, timeout=120)
     assert r1.returncode == 0, r1.stderr
-    rn = subprocess.run(base + ["--gpus", str(gpus), "--same-device", "--out", str(many)],
-                        capture_output=True, text=True, timeout=120)
+    rn = subprocess.run(base + ["--gpus", str(gpus)] + (["--same-device"] if same else []) +
+                        ["--out", str(many)], capture_output=True, text=True, timeout=120)
     assert rn.returncode == 0, rn.stderr
-    assert f"{gpus} renderers" in rn.stdout
+    assert f"{gpus} devices" in rn.stdout
+    assert ("transport peer" if same else "transport rccl") in rn.stdout
     assert one.read_bytes() == many.read_bytes()
 
 

@@ -28,7 +28,7 @@ from raytracingstudy_amd.camera import scene_pose  # noqa: E402
 
 # the shipped variants: 0 = default for the spp, 7 = block-tile queue counting
 # every frame, 10 = the spp < 8 default, 13 = the spp >= 8 default
-SHIPPED_VARIANTS = [0, 7, 10, 13]
+SHIPPED_VARIANTS = [0, 4, 7, 10, 13]
 CASES = [  # n, w, h, spp, depth
     (1000, 160, 120, 1, 7),
     (20000, 128, 96, 2, 12),

@@ -30,10 +30,29 @@ from raytracingstudy_amd.camera import scene_pose  # noqa: E402
 WAVE_WORDS = 65536 * 4
 
 
+def unit_gaps(u: np.ndarray) -> dict:
+    """Per wave (column 2's low 16 bits: workgroup * 4 + wave), the idle time
+    between one unit's end and the same wave's next unit's start: the
+    scheduler's cost per unit (dequeue, barriers, the pixel epilogue)."""
+    if u.shape[1] < 3 or not len(u):
+        return {}
+    wid = (u[:, 2] & 0xFFFF).astype(np.int64)
+    order = np.lexsort((u[:, 0], wid))
+    w, s, e = wid[order], u[order, 0], u[order, 1]
+    same = w[1:] == w[:-1]
+    gaps = (s[1:] - e[:-1])[same] / 100.0
+    if not len(gaps):
+        return {}
+    return {"gap_us": {p: round(float(np.percentile(gaps, q)), 2) for p, q in
+                       (("p10", 10), ("p50", 50), ("p90", 90), ("p99", 99))},
+            "gap_mean_us": round(float(gaps.mean()), 3), "gaps": int(len(gaps))}
+
+
 def summarise_units(u: np.ndarray, t0: int, span_us: float) -> dict:
     u = u[u[:, 1] > 0]
     if not len(u):
         return {"units": 0}  # this path records no per-unit times
+    gaps = unit_gaps(u)
     st = (u[:, 0] - t0) / 100.0
     du = (u[:, 1] - u[:, 0]) / 100.0
     en = st + du
@@ -49,7 +68,12 @@ def summarise_units(u: np.ndarray, t0: int, span_us: float) -> dict:
             "units_ending_last_10pct": int(late.sum()),
             "their_dur_p50_max_us": [round(float(np.median(du[late])), 1) if late.any() else 0,
                                      round(float(du[late].max()), 1) if late.any() else 0],
-            "their_start_min_us": round(float(st[late].min()), 1) if late.any() else 0}
+            "their_start_min_us": round(float(st[late].min()), 1) if late.any() else 0,
+            # share of the waves' launch span spent inside units (the rest:
+            # ramp, scheduling gaps, tail)
+            "in_unit_share": (round(float(du.sum()) / (len(np.unique(u[:, 2] & 0xFFFF)) * span_us), 3)
+                              if u.shape[1] > 2 else None),
+            **gaps}
 
 
 def summarise(rec: np.ndarray, unit_rec: np.ndarray) -> dict:
@@ -89,7 +113,7 @@ def main():
     r = rt.KernelRenderer(cfg.width, cfg.height, mode="scene", spp=cfg.spp, variant=args.variant)
     r.resize(cfg.width, cfg.height)
     r.setPosition(scene_pose())
-    r.set_scene(sp, al, max_depth=cfg.max_depth)
+    r.set_scene(sp, al, max_depth=cfg.max_depth, leaf_capacity=cfg.leaf_capacity)
     ts = rt.configs.TILE_SIZE
     share = T.tiles_for_rank(cfg.width, cfg.height, 0, args.n, ts)
     slab = torch.zeros(len(share) * ts * ts * 4, dtype=torch.uint8, device="cuda")
@@ -110,7 +134,7 @@ def main():
             dumps[name] = raw[:, WAVE_WORDS:unit_end].reshape(args.frames, -1, 3)
             dumps[name + "_waves"] = raw[:, :WAVE_WORDS].reshape(args.frames, -1, 4)
         for i in range(args.frames):
-            sm = summarise(raw[i, :WAVE_WORDS].reshape(-1, 4), raw[i, WAVE_WORDS:unit_end].reshape(-1, 3)[:, :2])
+            sm = summarise(raw[i, :WAVE_WORDS].reshape(-1, 4), raw[i, WAVE_WORDS:unit_end].reshape(-1, 3))
             ph = raw[i, unit_end:].reshape(-1, 2).sum(0).astype(float)
             sm["phase_ticks_share"] = {"primary": round(ph[0] / max(ph.sum(), 1), 3),
                                        "shadow": round(ph[1] / max(ph.sum(), 1), 3)}
