@@ -42,7 +42,7 @@ def main():
         with rt.KernelRenderer(c.width, c.height, mode="scene", spp=c.spp, variant=args.variant) as r:
             r.resize(c.width, c.height)
             r.setPosition(scene_pose())
-            r.set_scene(sp, al, max_depth=c.max_depth)
+            r.set_scene(sp, al, max_depth=c.max_depth, leaf_capacity=c.leaf_capacity)
             st = r.render(stats=True)
         rec = json.loads(open(path).read().strip().splitlines()[-1])
         os.unlink(path)
