@@ -263,11 +263,13 @@ def roofline(kern_ms: float, touched_bytes: float, pmc, simds: int, pmc_path: st
 
 
 def secondary_config(rt, torch, name: str, dev, stream, steps: int = 3, pmc_path: str = "",
-                     simds: int = 1024) -> dict:
+                     simds: int = 1024, min_s: float = 0.5, max_frames: int = 400) -> dict:
     """Time another BASELINE config on this GPU: kernel ms (HIP events on the
-    launch stream), Mrays/s from the counted rays, scene build time, and its
-    roofline when the PMC summary holds this config at this build's kernel
-    sources (profiles/pmc_latest.json, key = config name)."""
+    launch stream, the median of at least `steps` frames and of as many more
+    as fill `min_s` seconds, at most `max_frames`), Mrays/s from the counted
+    rays, scene build time, and its roofline when the PMC summary holds this
+    config at this build's kernel sources (profiles/pmc_latest.json, key =
+    config name)."""
     import numpy as np
     from raytracingstudy_amd.camera import scene_pose
 
@@ -281,7 +283,7 @@ def secondary_config(rt, torch, name: str, dev, stream, steps: int = 3, pmc_path
         st = r2.render(None, stream.cuda_stream, stats=True)
         rays = st.primary_rays + st.shadow_rays
         ms = []
-        for _ in range(steps):
+        while len(ms) < steps or (sum(ms) < 1e3 * min_s and len(ms) < max_frames):
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
@@ -302,7 +304,7 @@ def secondary_config(rt, torch, name: str, dev, stream, steps: int = 3, pmc_path
         return {"roofline": roof, "workload": f"{c.width}x{c.height}, {c.spp} spp, {c.n_spheres} {c.scene} spheres, "
                             f"max depth {info['max_depth']}",
                 "depth_reached": info["depth_reached"], "cell_table_depth": info["cell_table_depth"],
-                "kernel_ms": round(k, 3), "Mrays_s": round(rays / k / 1e3, 1),
+                "kernel_ms": round(k, 3), "frames": len(ms), "Mrays_s": round(rays / k / 1e3, 1),
                 "rays_per_frame": int(rays), "scene_build_ms": round(info["build_ms"], 2),
                 "octree_nodes": info["n_nodes"], "prim_refs": info["n_prim_refs"]}
     finally:
