@@ -26,7 +26,11 @@ not its f32 operation order:
   through rationals), against the oracle's stack walk: the same hit, t,
   sphere, nodes_visited and prims_tested on every nearest and any-hit ray,
   with mutants (popped records counted again, leaf lists reversed) shown
-  to differ.
+  to differ;
+* the per-pixel accumulation (rounds of 64 samples, pairwise sums, rounds in
+  order, x 1/spp; progressive frames continuing the stored sums) restated in
+  numpy float32 from DESIGN.md §2.2 over the oracle's per-sample colours,
+  bit for bit, with two other summation orders shown to differ.
 """
 from __future__ import annotations
 
@@ -675,3 +679,118 @@ def test_walk_spec_check_catches_mutants(oracle, mutant):
             _, _, _, cnt = sc.trace(o, dd, any_hit=anyh)
             diffs += (nodes, prims) != (int(cnt[2]), int(cnt[3]))
     assert diffs > 0
+
+
+# ---------------------------------------------------------------------------
+# Accumulation (DESIGN.md §2.2 "Accumulate"), restated in numpy float32 from
+# its text: rounds of spw = min(spp, 64) samples in sample order, each round
+# summed pairwise over g = pow2ceil(spw) slots (missing slots 0), round sums
+# added in order, then x (1/spp).  The per-sample colours come from the oracle
+# one sample at a time (a progressive frame k of 1 spp onto a zero sum holds
+# sample k's colour exactly: 0 + c == c), so this pins the summation order,
+# the rounds and the progressive continuation, not the shading.
+# ---------------------------------------------------------------------------
+
+def _spec_tree(v: np.ndarray) -> np.ndarray:
+    """T(v, n) = T(v, n/2) + T(v + n/2, n/2) over the first axis (n a power of
+    two), f32 at every add: level by level, adjacent pairs first (the
+    recursion's leaves), as a butterfly whose lane distance doubles."""
+    while v.shape[0] > 1:
+        v = (v[0::2] + v[1::2]).astype(np.float32)
+    return v[0]
+
+
+def _spec_accumulate(colours: np.ndarray, acc0=None) -> np.ndarray:
+    """colours (spp, h, w, 3) f32 in sample order -> the frame's f32 sum."""
+    spp = colours.shape[0]
+    spw = min(spp, 64)
+    g = 1
+    while g < spw:
+        g *= 2
+    acc = None if acc0 is None else acc0
+    for r0 in range(0, spp, spw):
+        rnd = np.zeros((g,) + colours.shape[1:], np.float32)
+        part = colours[r0:r0 + spw]
+        rnd[:part.shape[0]] = part
+        t = _spec_tree(rnd)
+        acc = t if acc is None else (acc + t).astype(np.float32)
+    return acc
+
+
+def _sample_colours(sc, w, h, pose, K, spp):
+    out = np.zeros((spp, h, w, 3), np.float32)
+    for k in range(spp):
+        acc = np.zeros((h, w, 4), np.float32)
+        sc.render(w, h, pose, K, spp=1, jitter=True, frame=k, accum=acc)
+        out[k] = acc[..., :3]
+    return out
+
+
+@pytest.mark.parametrize("spp", [12, 64, 100, 256])
+def test_accumulation_matches_spec(oracle, spp):
+    """The oracle's per-pixel sums (the GPU reproduces them bit for bit) equal
+    the spec's rounds of pairwise sums, for a sub-64 count (12: one round of
+    16 slots), one full round (64), a ragged second round (100: 64 + 36 in 64
+    slots) and four rounds (256, the sorted path's count)."""
+    w, h = 24, 16
+    sp, al = spec_spheres(3000)
+    pose = scene_pose()
+    K = oracle.resize_intrinsic(w, h)
+    sc = oracle.Scene(sp, al)
+    cols = _sample_colours(sc, w, h, pose, K, spp)
+    acc = _spec_accumulate(cols)
+    # the frame of spp samples at frame 0 (no accumulation buffer) uses the
+    # same sample indices 0..spp-1
+    ref8, rad, _ = sc.render(w, h, pose, K, spp=spp)
+    mean = (acc * (np.float32(1.0) / np.float32(spp))).astype(np.float32)  # 1.0f / spp in f32
+    assert np.array_equal(rad[..., :3], mean)
+    px = np.floor(np.clip(mean, 0, 1) * np.float32(255.0)).astype(np.uint8)
+    assert np.array_equal(ref8[..., :3], px)
+    # the order matters at f32: a plain running sum in sample order, and a
+    # pairing of the two halves' slots first (lane distance halving), differ
+    plain = np.zeros((h, w, 3), np.float32)
+    for c in cols:
+        plain = (plain + c).astype(np.float32)
+    assert not np.array_equal(plain, acc)
+
+    def halves_first(v):
+        while v.shape[0] > 1:
+            v = (v[:v.shape[0] // 2] + v[v.shape[0] // 2:]).astype(np.float32)
+        return v[0]
+    g = 1
+    while g < min(spp, 64):
+        g *= 2
+    mut = None
+    for r0 in range(0, spp, min(spp, 64)):
+        rnd = np.zeros((g, h, w, 3), np.float32)
+        part = cols[r0:r0 + min(spp, 64)]
+        rnd[:part.shape[0]] = part
+        t = halves_first(rnd)
+        mut = t if mut is None else (mut + t).astype(np.float32)
+    assert not np.array_equal(mut, acc)
+
+
+def test_progressive_accumulation_matches_spec(oracle):
+    """Progressive frames (F3): frame k of S samples adds its rounds onto the
+    stored sum and is scaled by 1/((k+1)S); three frames of 64 equal the spec
+    applied to samples 0..191 frame by frame, and the stored sum equals one
+    192-sample frame's only where the spec says the rounds line up."""
+    w, h, S = 24, 16, 64
+    sp, al = spec_spheres(3000)
+    pose = scene_pose()
+    K = oracle.resize_intrinsic(w, h)
+    sc = oracle.Scene(sp, al)
+    cols = _sample_colours(sc, w, h, pose, K, 3 * S)
+    acc = np.zeros((h, w, 4), np.float32)
+    spec = None
+    for k in range(3):
+        _, rad, _ = sc.render(w, h, pose, K, spp=S, jitter=True, frame=k, accum=acc)
+        spec = _spec_accumulate(cols[k * S:(k + 1) * S], spec)
+        assert np.array_equal(acc[..., :3], spec)
+        mean = (spec * (np.float32(1.0) / np.float32((k + 1) * S))).astype(np.float32)
+        assert np.array_equal(rad[..., :3], mean)
+    # rounds of 64 line up with the frames, so three 64-sample frames sum
+    # exactly like one 192-sample frame
+    _, rad192, _ = sc.render(w, h, pose, K, spp=3 * S)
+    assert np.array_equal(rad192[..., :3],
+                          (spec * (np.float32(1.0) / np.float32(3 * S))).astype(np.float32))
