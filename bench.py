@@ -280,6 +280,7 @@ def secondary_config(rt, torch, name: str, dev, stream, steps: int = 3, pmc_path
         r2.resize(c.width, c.height)
         r2.setPosition(scene_pose())
         info = r2.set_scene(sp, al, max_depth=c.max_depth, leaf_capacity=c.leaf_capacity)
+        rebuild = r2.set_scene(sp, al, max_depth=c.max_depth, leaf_capacity=c.leaf_capacity)
         st = r2.render(None, stream.cuda_stream, stats=True)
         rays = st.primary_rays + st.shadow_rays
         ms = []
@@ -306,6 +307,7 @@ def secondary_config(rt, torch, name: str, dev, stream, steps: int = 3, pmc_path
                 "depth_reached": info["depth_reached"], "cell_table_depth": info["cell_table_depth"],
                 "kernel_ms": round(k, 3), "frames": len(ms), "Mrays_s": round(rays / k / 1e3, 1),
                 "rays_per_frame": int(rays), "scene_build_ms": round(info["build_ms"], 2),
+                "scene_rebuild_ms": round(rebuild["build_ms"], 2),
                 "octree_nodes": info["n_nodes"], "prim_refs": info["n_prim_refs"]}
     finally:
         r2.close()
@@ -347,6 +349,9 @@ def main():
     pose = scene_pose()
     r.setPosition(pose)
     info = r.set_scene(sp, al, max_depth=cfg.max_depth, leaf_capacity=cfg.leaf_capacity)
+    # the same scene again: a rebuild into the buffers the first build sized
+    # (the per-frame cost of a dynamic scene; the first build also allocates)
+    rebuild = r.set_scene(sp, al, max_depth=cfg.max_depth, leaf_capacity=cfg.leaf_capacity)
     _, K = r.camera()
 
     dev = torch.device("cuda", local)
@@ -546,6 +551,7 @@ def main():
                 "render_span_ms": round(kern_ms, 4),
                 "wall_ms_per_step": round(elapsed / args.steps * 1e3, 4),
                 "scene_build_ms": round(info["build_ms"], 1),
+                "scene_rebuild_ms": round(rebuild["build_ms"], 2),
                 "scene_upload_ms": round(info["upload_ms"], 1),
             },
             "roofline": roof,
