@@ -469,11 +469,12 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 const uint32_t n0 = e0 == texit ? l0 + size : l0;
                 const uint32_t n1 = e1 == texit ? l1 + size : l1;
                 const uint32_t n2 = e2 == texit ? l2 + size : l2;
-                // leave on an any-hit, a nearest hit before this cell's exit, the
-                // ray's end, or the root's boundary (the same order of tests as
-                // the oracle, whose results do not depend on that order)
-                stop = any_hit | (!kAnyHit & (best_t < texit)) | (texit >= t1) |
-                       ((n0 | n1 | n2) >= G);
+                // leave on an any-hit, a nearest hit before this cell's exit, or
+                // the ray's end.  The oracle's root-boundary test (a stepped
+                // coordinate reaching G) needs no term of its own: an axis that
+                // steps to G exits through plane(i, G), the very value t1 is
+                // the minimum of, so texit >= t1 already holds there.
+                stop = any_hit | (!kAnyHit & (best_t < texit)) | (texit >= t1);
                 const uint32_t diff = (l0 ^ n0) | (l1 ^ n1) | (l2 ^ n2);
                 const uint32_t top = 31u - __builtin_clz(diff);  // highest flipped bit
                 t = texit;
