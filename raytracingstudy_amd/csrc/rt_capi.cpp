@@ -1275,7 +1275,9 @@ int multi_synchronize(rt_renderer* r) {
     for (size_t k = 0; k < m.devs.size(); ++k) {
         RT_HIP(r, hipSetDevice(m.devs[k]));
         if (m.cs[k]) RT_HIP(r, hipStreamSynchronize(m.cs[k]));
+        // (a creation that failed part-way leaves later peers unmade)
         rt_renderer* p = m.peers[k];
+        if (!p) continue;
         RT_HIP(r, hipStreamSynchronize(p->stream));
         if (p->pending) RT_HIP(r, hipEventSynchronize(p->done));
     }
