@@ -2,10 +2,17 @@
 """Headline benchmark: Mrays/s (primary + shadow) and ms/frame, 1/2/4/8 GPUs.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
-    torchrun --nproc-per-node N bench.py --gpus N ...
+    torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
+    python bench.py --gpus N                              (N > 1: one process, N GPUs)
 
 A step is one frame of the BASELINE config (default C3: 1920x1080, 64 spp,
-100k spheres, depth-7 octree).  N=1 renders the whole frame; N>1 deals 64x64
+100k spheres, depth-7 octree).  `--gpus N` measures N GPUs however it is
+launched (launch_mode): under torchrun the world must be N (else exit 2);
+without a launcher N > 1 (or --native) drives the N devices from this one
+process through the C-ABI's multi-device handle, rt_create_multi, which the
+reference's Displayer would call (run_native: RCCL ncclCommInitAll, grouped
+send/recv, one unpack); N > visible GPUs exits 2.  N=1 renders the whole
+frame.  Under torchrun, N>1 deals 64x64
 tiles round-robin over the ranks, each rank renders its tiles
 into a packed slab, the slabs are gathered to rank 0 over RCCL and unpacked
 into the frame there — the gather is inside the timed step.  The frame is the
@@ -46,7 +53,7 @@ L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s over the
 VMEM_CHARGE_BYTES = 64 * 16
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     # ~2 s of timed frames at N = 1 (9.3 ms each): long enough for an outside
@@ -78,7 +85,53 @@ def parse():
                          "under `secondary`; '' to skip")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="PMC traffic summary written by tools/pmc_traffic.py")
-    return ap.parse_args()
+    ap.add_argument("--native", action="store_true",
+                    help="drive the N GPUs from this one process through the C-ABI's multi-device "
+                         "handle (rt_create_multi: tiles round-robin, RCCL gather, one unpack), the "
+                         "path the reference's Displayer calls; the default without a launcher at N > 1")
+    ap.add_argument("--transport", default="auto", choices=("auto", "rccl", "peer"),
+                    help="--native: slab transport (auto = RCCL for distinct devices)")
+    return ap.parse_args(argv)
+
+
+class stdout_to_stderr:
+    """Send file descriptor 1 to stderr for a block: RCCL's version banner and
+    gloo's connection messages are printed from C++ on stdout, where the
+    bench's one JSON line must be the only output."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
+def launch_mode(gpus: int, native: bool, env) -> tuple:
+    """Which path `--gpus N` measures: ("single" | "torchrun" | "native", None),
+    or (None, why) when the launch cannot measure N GPUs as asked.
+
+    * under torchrun (WORLD_SIZE set) the world must be N: one process per GPU,
+      the tile path with the RCCL gather (N > 1) or the whole frame (N = 1);
+    * without a launcher, N > 1 (or --native) drives N devices from this one
+      process through rt_create_multi, as the reference's Displayer would;
+    * N = 1 without a launcher renders whole frames on one GPU."""
+    if gpus < 1:
+        return None, f"--gpus {gpus}: at least 1"
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            return None, (f"--gpus {gpus} but WORLD_SIZE={ws}: launch torchrun with "
+                          f"--nproc-per-node {gpus}, or run without a launcher for the native path")
+        if native:
+            return None, "--native drives every GPU from one process: run it without torchrun"
+        return ("torchrun" if gpus > 1 else "single"), None
+    return ("native" if native or gpus > 1 else "single"), None
 
 
 def cpu_baseline(cfg, K, pose, target_s: float) -> dict:
@@ -138,6 +191,44 @@ def load_pmc(path: str, cfg_name: str, world: int, src_id: str, leaf_capacity: i
         return None, (f"PMC summary taken at leaf capacity {ent.get('leaf_capacity', 8)}, "
                       f"the config builds {leaf_capacity}: stale, not used")
     return ent, "ok"
+
+
+# per-launch counts of a PMC summary that scale with the work a launch does
+# (a rank's share of the frame); fractions, the clock and lane use do not
+PMC_PER_LAUNCH = ("hbm_bytes_per_launch", "valu_insts_per_launch", "vmem_rd_insts_per_launch",
+                  "vmem_wr_insts_per_launch", "tcp_cache_accesses_per_launch")
+
+
+def project_pmc(ent: dict, share: float, note: str) -> dict:
+    """The N=1 PMC entry of a config projected onto a launch that does `share`
+    of the frame's work (N>1 lines had no PMC roofs).
+    Per-launch counts are scaled by the share; busy fractions (TD, TA), the
+    clock and lane utilisation are kept as measured at N=1.  The result says
+    so in `projected`, which roofline() copies into the line."""
+    p = dict(ent)
+    for k in PMC_PER_LAUNCH:
+        if p.get(k) is not None:
+            p[k] = float(p[k]) * share
+    if isinstance(p.get("sq"), dict):
+        p["sq"] = {k: (float(v) * share if k.startswith("SQ_INSTS") else v) for k, v in p["sq"].items()}
+    p["projected"] = note
+    return p
+
+
+def pmc_for_launch(path: str, cfg, world: int, src_id: str, share: float):
+    """(PMC entry, note) for a launch doing `share` of `cfg`'s frame on one of
+    `world` GPUs: the entry measured at that GPU count if the summary has one,
+    else the N=1 entry projected by the share (project_pmc)."""
+    ent, note = load_pmc(path, cfg.name, world, src_id, cfg.leaf_capacity)
+    if ent is not None and share >= 0.999999:
+        return ent, note
+    ent1, note1 = load_pmc(path, cfg.name, 1, src_id, cfg.leaf_capacity)
+    if ent1 is None:
+        return None, note1
+    return project_pmc(ent1, share,
+                       f"projected from the N=1 counters of {cfg.name} (the whole-frame kernel), per-launch "
+                       f"counts scaled by this launch's share of the frame's rays ({share:.4f}); busy "
+                       f"fractions, clock and lane use as measured at N=1"), "projected"
 
 
 def roofline(kern_ms: float, touched_bytes: float, pmc, simds: int, pmc_path: str = "",
@@ -259,6 +350,8 @@ def roofline(kern_ms: float, touched_bytes: float, pmc, simds: int, pmc_path: st
     out["roofs"] = roofs
     if not pmc:
         out["pmc"] = pmc_note
+    elif pmc.get("projected"):
+        out["pmc_projected"] = pmc["projected"]
     return out
 
 
@@ -313,8 +406,147 @@ def secondary_config(rt, torch, name: str, dev, stream, steps: int = 3, pmc_path
         r2.close()
 
 
+def run_native(args) -> int:
+    """`--gpus N` without a launcher: ONE process drives N devices through the
+    C-ABI's multi-device handle (rt_create_multi; SURVEY 8e E1 "one process,
+    8 devices, ncclCommInitAll"), the path the reference's Displayer calls
+    (src/window/displayer.cpp:28,51).  A step is one rt_render
+    of the whole frame: every device renders its round-robin 64x64 tiles into
+    a slab, the slabs travel to devices[0] (grouped ncclSend / ncclRecv, or
+    peer copies) and ONE unpack assembles the frame; two frames are in flight
+    inside the handle.  The K timed steps run back to back, bracketed by
+    rt_synchronize (every device's streams); ms per step is wall time, with
+    HIP events on devices[0]'s output stream beside it."""
+    import numpy as np
+    import torch
+
+    import raytracingstudy_amd as rt
+    from raytracingstudy_amd.camera import scene_pose
+
+    cfg = rt.CONFIGS[args.config]
+    if cfg.mode != "scene":
+        raise SystemExit("bench runs a scene config (c2..c5)")
+    n = args.gpus
+    seen = rt.device_count()
+    devs = [0] * n if args.same_device else list(range(n))
+    if max(devs) >= seen:
+        print(f"bench.py: --gpus {n} needs {n} visible GPUs, {seen} visible "
+              f"(--same-device rehearses the plan on GPU 0)", file=sys.stderr)
+        return 2
+    W, H, ts = cfg.width, cfg.height, rt.configs.TILE_SIZE
+    sp, al = rt.configs.scene_spheres(cfg, rt.SEED)
+    pose = scene_pose()
+    kw = dict(mode="scene", spp=cfg.spp, light_dir=rt.configs.LIGHT_DIR, ambient=rt.configs.AMBIENT,
+              variant=args.variant)
+    with stdout_to_stderr():  # ncclCommInitAll prints RCCL's banner
+        r = rt.KernelRenderer(W, H, devices=devs, transport=args.transport, **kw)
+    r.resize(W, H)
+    r.setPosition(pose)
+    info = r.set_scene(sp, al, max_depth=cfg.max_depth, leaf_capacity=cfg.leaf_capacity)
+    rebuild = r.set_scene(sp, al, max_depth=cfg.max_depth, leaf_capacity=cfg.leaf_capacity)
+    st = r.render(stats=True)  # counters summed over the devices (equal to the oracle's)
+    rays_frame = st.primary_rays + st.shadow_rays
+    for _ in range(args.warmup):
+        r.render()
+    r.synchronize()
+    dev0 = torch.device("cuda", devs[0])
+    out_stream = torch.cuda.ExternalStream(r.stream_ptr(), device=dev0)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(out_stream)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r.render()
+    e1.record(out_stream)
+    r.synchronize()
+    elapsed = time.perf_counter() - t0
+    ev_ms = e0.elapsed_time(e1)
+    # outside the timed region: per-device times of single frames (the
+    # handle waits after each), the frame against one renderer's whole frame,
+    # and devices[0]'s own tiles rendered alone for its counters
+    per = []
+    for _ in range(5):
+        r.render()
+        per.append(r.multi_timing())
+    mi = r.multi_info()
+    img = r.readback()
+    r.close()
+    ref = rt.KernelRenderer(W, H, device=devs[0], **kw)
+    ref.resize(W, H)
+    ref.setPosition(pose)
+    ref.set_scene(sp, al, max_depth=cfg.max_depth, leaf_capacity=cfg.leaf_capacity)
+    ref.render()
+    frame_ok = bool(np.array_equal(ref.readback(), img))
+    T = -(-W // ts) * -(-H // ts)
+    ids0 = [t for t in range(T) if t % n == 0]
+    slab = torch.empty(len(ids0) * ts * ts * 4, dtype=torch.uint8, device=dev0)
+    s0 = ref.render_tiles(ids0, ts, slab.data_ptr(), stats=True)
+    ref.close()
+    render_ms = [float(np.median([p["render_ms"][k] for p in per])) for k in range(n)]
+    deliver_ms = float(np.median([p["deliver_ms"] for p in per]))
+    rays0 = s0.primary_rays + s0.shadow_rays
+    alg0 = s0.nodes_visited * NODE_BYTES + s0.prims_tested * PRIM_BYTES + len(ids0) * ts * ts * PIXEL_BYTES
+    simds = torch.cuda.get_device_properties(dev0).multi_processor_count * 4
+    pmc, note = pmc_for_launch(args.pmc, cfg, n, rt._lib.kernel_source_id(), rays0 / rays_frame)
+    roof = roofline(render_ms[0], alg0, pmc, simds, args.pmc, note)
+    if pmc and pmc.get("valu_lane_util") is not None:
+        roof["valu_lane_util"] = round(pmc["valu_lane_util"], 4)
+    roof["time_ms"] = round(render_ms[0], 4)
+    roof["time_source"] = ("devices[0]'s render of its tiles, HIP events on its render stream "
+                           "(rt_get_multi_timing, median of 5 single frames)")
+    roof["per_ray"] = {"nodes": s0.nodes_visited / rays0, "prims": s0.prims_tested / rays0}
+    value = rays_frame * args.steps / elapsed / 1e6
+    out = {
+        "metric": f"Mrays/s (primary+shadow) at {W}x{H}, {cfg.spp} spp, {cfg.n_spheres} spheres",
+        "value": round(value, 3),
+        "unit": "Mrays/s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded spheres, SURVEY.md 8d)",
+        "config": {
+            "workload": f"{cfg.name}: {cfg.note}",
+            "width": W, "height": H, "spp": cfg.spp, "n_spheres": cfg.n_spheres,
+            "octree_depth": info["max_depth"], "octree_nodes": info["n_nodes"],
+            "prim_refs": info["n_prim_refs"], "leaf_capacity": cfg.leaf_capacity,
+            "parallelism": f"native-tiles{ts}x{n}",
+            "launch": "native: one process, rt_create_multi over devices " + str(mi["devices"]),
+            "transport": mi["transport"],
+            "devices_seen": seen,
+            "frames_in_flight": mi["frames_in_flight"],
+            "rays_per_frame": int(rays_frame),
+            "primary_per_frame": int(st.primary_rays), "shadow_per_frame": int(st.shadow_rays),
+            "wall_ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "event_ms_per_step": round(ev_ms / args.steps, 4),
+            "device_render_ms": [round(x, 4) for x in render_ms],
+            "deliver_ms": round(deliver_ms, 4),
+            "tiles_frame_check": frame_ok,
+            "scene_build_ms": round(info["build_ms"], 1),
+            "scene_rebuild_ms": round(rebuild["build_ms"], 2),
+            "scene_upload_ms": round(info["upload_ms"], 1),
+        },
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+    if args.same_device:
+        out["config"]["note"] = ("rehearsal: every device is GPU 0, so the per-device render times "
+                                 "include the other devices' kernels")
+    print(json.dumps(out), flush=True)
+    return 0 if frame_ok else 1
+
+
 def main():
     args = parse()
+    mode, why = launch_mode(args.gpus, args.native, os.environ)
+    if mode is None:
+        print(f"bench.py: {why}", file=sys.stderr)
+        sys.exit(2)
+    if mode == "native":
+        sys.exit(run_native(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -331,12 +563,18 @@ def main():
         if args.backend != "gloo":
             raise SystemExit("--same-device is a gloo rehearsal (RCCL needs one GPU per rank)")
         local = 0
+    elif local >= torch.cuda.device_count():
+        print(f"bench.py: rank {rank} needs GPU {local}, {torch.cuda.device_count()} visible",
+              file=sys.stderr)
+        sys.exit(2)
     torch.cuda.set_device(local)
     if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
+        with stdout_to_stderr():  # RCCL's banner, gloo's connection messages
+            if args.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group("gloo")
+            dist.barrier()
     cfg = rt.CONFIGS[args.config]
     if cfg.mode != "scene":
         raise SystemExit("bench runs a scene config (c2..c5)")
@@ -449,11 +687,12 @@ def main():
     cnt = torch.tensor([st.primary_rays, st.shadow_rays, st.nodes_visited, st.prims_tested],
                        dtype=torch.float64, device=dev)
 
-    for i in range(args.warmup):
-        step(i, False)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    with stdout_to_stderr():  # a collective's first use may print too
+        for i in range(args.warmup):
+            step(i, False)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -510,13 +749,21 @@ def main():
         pix = (W * H) if not tiled else len(my_ids) * ts * ts
         alg_bytes = float(cnt[2].item()) * NODE_BYTES + float(cnt[3].item()) * PRIM_BYTES + pix * PIXEL_BYTES
         simds = torch.cuda.get_device_properties(dev).multi_processor_count * 4
-        pmc, pmc_note = load_pmc(args.pmc, cfg.name, world, rt._lib.kernel_source_id(),
-                                 cfg.leaf_capacity)
+        src_id = rt._lib.kernel_source_id()
+        if not tiled:
+            pmc, pmc_note = load_pmc(args.pmc, cfg.name, world, src_id, cfg.leaf_capacity)
+        elif args.shard:
+            pmc, pmc_note = None, "--shard projection: no PMC roofs"
+        else:
+            # the tile path: this rank's launch does its share of the frame's
+            # rays; the N=1 counters projected onto it
+            share = float(cnt[0].item() + cnt[1].item()) / rays_frame
+            pmc, pmc_note = pmc_for_launch(args.pmc, cfg, world, src_id, share)
         # frames in flight overlap, so one frame's event span is not its share
         # of the GPU: price a frame per step of wall time instead
         roof_ms = kern_ms if F == 1 else elapsed / args.steps * 1e3
-        roof = roofline(roof_ms, alg_bytes, pmc if not tiled else None, simds, args.pmc, pmc_note)
-        if pmc and pmc.get("valu_lane_util") is not None and not tiled:
+        roof = roofline(roof_ms, alg_bytes, pmc, simds, args.pmc, pmc_note)
+        if pmc and pmc.get("valu_lane_util") is not None:
             roof["valu_lane_util"] = round(pmc["valu_lane_util"], 4)
         roof["time_ms"] = round(roof_ms, 4)
         roof["time_source"] = ("kernel HIP events on the launch stream" if F == 1 else

@@ -30,8 +30,8 @@
  *   cudaGraphicsResourceGetMappedPointer + unmap          rt_render(dev_rgba8 = mapped ptr)
  *     src/renderer.cu:145-151
  *   (none: single device)                                 rt_render_tiles / rt_unpack_tiles
- *   (none: single device; SURVEY 8b B2 "device ids",      rt_create_multi / rt_get_multi_info
- *     8e E1 ncclCommInitAll)
+ *   (none: single device; SURVEY 8b B2 "device ids",      rt_create_multi / rt_get_multi_info /
+ *     8e E1 ncclCommInitAll)                                rt_get_multi_timing
  *   (none: no error reporting, all void)                  rt_last_error
  *
  * Threading: one handle per host thread / stream; calls on one handle are not
@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 typedef struct rt_renderer rt_renderer;
 
@@ -279,7 +279,8 @@ int rt_readback(rt_renderer* r, uint8_t* host_rgba8, float* host_rgba32f);
 /* Device pointer of the internal framebuffer (W*H*4 bytes). */
 void* rt_framebuffer(rt_renderer* r);
 /* The renderer's own stream (a hipStream_t made with the handle), the one a
- * NULL stream argument means.  Extension: the reference launches on the legacy
+ * NULL stream argument means (a multi-device handle: its output stream on
+ * devices[0]).  Extension: the reference launches on the legacy
  * default stream (src/renderer.cu:149).  Renderers made one after another get
  * streams on different hardware queues, so frames in flight on them overlap. */
 void* rt_stream(rt_renderer* r);
@@ -322,9 +323,33 @@ typedef struct rt_multi_info {
     uint32_t frames_in_flight;       /* 2                                                 */
     uint64_t frames;                 /* frames rendered by the handle                     */
 } rt_multi_info;
+/* Refuses RT_FLAG_RADIANCE (RT_E_INVALID: the slabs carry RGBA8 only).  The
+ * tile plan and its slabs are allocated here for cfg's size (again at the
+ * first frame after a resize), so an allocation failure is reported by this
+ * call.  A NULL stream argument (rt_render, rt_stream) means the handle's
+ * output stream on devices[0], which is not devices[0]'s render stream, so
+ * frame j+1's tiles there do not wait for frame j's unpack.  A failure on one
+ * device names it in rt_last_error: "(device <ordinal>, peer <k>)".
+ * Test-only: the environment variable RT_TEST_FAULT, read here, injects one
+ * failure: "create:k" (peer k's renderer), "comm" (ncclCommInitAll), "slab:k"
+ * (peer k's slab allocation) or "queue:k" (peer k's frames flag their
+ * wave-queue error, which rt_synchronize / rt_readback report as RT_E_HIP). */
 int rt_create_multi(const rt_config* cfg, const int32_t* devices, uint32_t n_devices,
                     uint32_t transport, rt_renderer** out);
 int rt_get_multi_info(const rt_renderer* r, rt_multi_info* info);
+/* Device times of the handle's last frame (waits for the handle's queued
+ * work): render_ms[k] = device k rendering its tiles into its slab (HIP
+ * events on its render stream); deliver_ms = on devices[0], from the end of
+ * its own tiles to the frame unpacked (the other slabs' arrival over the
+ * transport, then the one unpack).  RT_E_STATE for a single-device handle or
+ * before the first frame. */
+typedef struct rt_multi_timing {
+    uint32_t n_devices;
+    uint64_t frame;                   /* 0-based index of the frame timed           */
+    float render_ms[RT_MAX_DEVICES];
+    float deliver_ms;
+} rt_multi_timing;
+int rt_get_multi_timing(rt_renderer* r, rt_multi_timing* t);
 
 /* ---- errors --------------------------------------------------------------- */
 /* Last error message for this handle (r may be NULL: last global error). */

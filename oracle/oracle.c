@@ -473,6 +473,42 @@ static inline int isect(const float o[3], const float d[3], const float* sp, flo
     return 1;
 }
 
+/* Test-only check of the PRODUCT's camera-relative screen (not part of the
+ * spec: the screen decides only which chunks run the exact tests, DESIGN.md
+ * 5.1).  Pair k is ray (o, dirs[3k..]) against sphere sp[4 idx[k]..]: the
+ * screen record is {o - c in f32, C' = |o - c|^2 - r^2 - slack_oc u |o - c|^2
+ * - slack_r u r^2 in f64 rounded toward -inf}, u = 2^-24 (rt_kernels.hip
+ * cam_screen_kernel), and the screen passes iff !(fmaf(b, b, -C') < 0) with b
+ * isect's b.  out[0] = pairs isect's discriminant accepts (h >= 0) that the
+ * screen rejects (a sound screen has none), out[1] = pairs the screen passes,
+ * out[2] = pairs with h >= 0. */
+void orc_cam_screen_check(const float o[3], const float* dirs, const float* sp, const uint32_t* idx,
+                          uint32_t m, double slack_oc, double slack_r, uint64_t out[3]) {
+    const double u = 1.0 / 16777216.0;
+    out[0] = out[1] = out[2] = 0;
+    for (uint32_t k = 0; k < m; ++k) {
+        const float* d = dirs + 3u * k;
+        const float* s = sp + 4u * idx[k];
+        const float ocx = o[0] - s[0], ocy = o[1] - s[1], ocz = o[2] - s[2];
+        const float b = fmaf(ocz, d[2], fmaf(ocy, d[1], ocx * d[0]));
+        const float qx = fmaf(-b, d[0], ocx);
+        const float qy = fmaf(-b, d[1], ocy);
+        const float qz = fmaf(-b, d[2], ocz);
+        const float qq = fmaf(qz, qz, fmaf(qy, qy, qx * qx));
+        const float h = fmaf(s[3], s[3], -qq);
+        const double oo = (double)ocx * ocx + (double)ocy * ocy + (double)ocz * ocz;
+        const double rr = (double)s[3] * s[3];
+        const double cd = oo - rr - slack_oc * u * oo - slack_r * u * rr;
+        float c = (float)cd;
+        if ((double)c > cd) c = nextafterf(c, -INFINITY);  /* toward -inf */
+        const int pass = !(fmaf(b, b, -c) < 0.0f);
+        const int exact = !(h < 0.0f);
+        out[0] += (uint64_t)(exact && !pass);
+        out[1] += (uint64_t)pass;
+        out[2] += (uint64_t)exact;
+    }
+}
+
 /* ---- octree walk (DESIGN.md "Octree walk") --------------------------------- */
 
 typedef struct {

@@ -142,6 +142,21 @@ class RtMultiInfo(ctypes.Structure):
                 "frames_in_flight": int(self.frames_in_flight), "frames": int(self.frames)}
 
 
+class RtMultiTiming(ctypes.Structure):
+    _fields_ = [
+        ("n_devices", ctypes.c_uint32),
+        ("frame", ctypes.c_uint64),
+        ("render_ms", ctypes.c_float * 16),
+        ("deliver_ms", ctypes.c_float),
+    ]
+
+    def as_dict(self) -> dict:
+        n = int(self.n_devices)
+        return {"n_devices": n, "frame": int(self.frame),
+                "render_ms": [round(float(self.render_ms[i]), 4) for i in range(n)],
+                "deliver_ms": round(float(self.deliver_ms), 4)}
+
+
 class RtDisplayOps(ctypes.Structure):
     _fields_ = [("map", DISPLAY_MAP), ("unmap", DISPLAY_UNMAP)]
 
@@ -185,6 +200,7 @@ SIGNATURES = {
     "rt_create_multi": (_int, [ctypes.POINTER(RtConfig), ctypes.POINTER(ctypes.c_int32), _u32, _u32,
                                ctypes.POINTER(_P)]),
     "rt_get_multi_info": (_int, [_P, ctypes.POINTER(RtMultiInfo)]),
+    "rt_get_multi_timing": (_int, [_P, ctypes.POINTER(RtMultiTiming)]),
 }
 
 _lock = threading.Lock()

@@ -32,6 +32,8 @@ bool variant_available(uint32_t v);
 hipError_t launch_unpack(const uint32_t* packed, const uint32_t* tiles, uint32_t n_tiles,
                          uint32_t ts, uint32_t tiles_x, uint32_t W, uint32_t H, uint32_t* img,
                          hipStream_t st);
+hipError_t launch_cam_screen(const float4* prim_sp, uint32_t n, const float o[3], float4* out,
+                             hipStream_t st);
 }  // namespace rtamd
 
 using namespace rtamd;
@@ -46,14 +48,29 @@ struct MultiState {
     uint32_t transport = 0;                // RT_TRANSPORT_RCCL / RT_TRANSPORT_PEER
     std::vector<ncclComm_t> comms;         // one per device (ncclCommInitAll)
     std::vector<hipStream_t> cs;           // per-device comm stream
+    // devices[0]'s output stream: what a NULL stream argument means for the
+    // handle (rt_stream).  Not devices[0]'s render stream, so that the wait
+    // for frame j's unpack does not hold frame j+1's tiles on device 0.
+    hipStream_t out = nullptr;
     // per frame slot f: each device's packed slab, devices[0]'s receive buffer
-    // of n slabs end to end, and the events that order their reuse
+    // of n slabs end to end, and the events that order their reuse (started /
+    // rendered / unpacked also time the frame: rt_get_multi_timing)
     std::vector<void*> slab[F];
     void* recv[F] = {nullptr, nullptr};
-    std::vector<hipEvent_t> rendered[F], sent[F];
+    std::vector<hipEvent_t> started[F], rendered[F], sent[F];
     hipEvent_t recvd[F] = {nullptr, nullptr}, unpacked[F] = {nullptr, nullptr}, out_ready = nullptr;
     bool used[F] = {false, false};
     uint64_t frame = 0;
+    // a resize that failed part-way leaves the devices at different sizes:
+    // rt_render refuses the handle until a resize succeeds
+    bool broken = false;
+    // test-only fault injection (RT_TEST_FAULT, read once by rt_create_multi):
+    // "create:k" peer k's rt_create fails, "comm" ncclCommInitAll fails,
+    // "slab:k" the slab allocation on peer k fails, "queue:k" peer k's frames
+    // flag their wave-queue error word (as a slot that was never published)
+    enum Fault { kNone = 0, kCreate, kComm, kSlab, kQueue };
+    int fault = kNone;
+    uint32_t fault_k = 0;
     // tile plan for the current size
     uint32_t W = 0, H = 0, S = 0;          // S = slab tiles
     size_t slab_bytes = 0;
@@ -131,6 +148,11 @@ struct rt_renderer {
     DevBuf<float4> d_spheres;
     DevBuf<uint32_t> d_albedo;
     SceneArgs sc{};
+    // camera-relative screen records (SceneArgs::prim_cam) and what they were
+    // made for: the scene build and the camera origin
+    DevBuf<float4> d_prim_cam;
+    uint64_t scene_gen = 0, cam_gen = ~0ull;
+    float cam_o[3] = {0.f, 0.f, 0.f};
     rt_scene_info info{};
     std::string err;
     // multi-device handle (rt_create_multi): this renderer is devices[0]'s
@@ -142,9 +164,14 @@ namespace {
 
 // multi-device handle internals (defined with rt_create_multi below)
 int multi_render(rt_renderer* r, uint32_t* out, hipStream_t hs, rt_stats* stats);
+int multi_wait(rt_renderer* r);
 int multi_synchronize(rt_renderer* r);
 void multi_destroy(rt_renderer* r);
 int multi_set_scene_device(rt_renderer* r, uint32_t n, const rt_octree_params* oct);
+// " (device <ordinal>, peer <k>)": names the device in a multi-device error
+std::string peer_name(const MultiState& m, size_t k) {
+    return " (device " + std::to_string(m.devs[k]) + ", peer " + std::to_string(k) + ")";
+}
 // apply `fn` to every other device's renderer of a multi-device handle
 template <typename Fn>
 int for_peers(rt_renderer* r, Fn fn) {
@@ -152,12 +179,15 @@ int for_peers(rt_renderer* r, Fn fn) {
     for (size_t k = 1; k < r->multi->peers.size(); ++k) {
         const int st = fn(r->multi->peers[k]);
         if (st) {
-            r->err = r->multi->peers[k]->err + " (device " + std::to_string(r->multi->devs[k]) + ")";
+            r->err = r->multi->peers[k]->err + peer_name(*r->multi, k);
             return st;
         }
     }
     return RT_OK;
 }
+// the stream a NULL stream argument means: the renderer's own, or a
+// multi-device handle's output stream on devices[0]
+hipStream_t own_stream(const rt_renderer* r) { return r->multi ? r->multi->out : r->stream; }
 
 int fail(rt_renderer* r, int code, const std::string& msg) {
     g_last_error = msg;
@@ -414,6 +444,7 @@ int build_scene(rt_renderer* r) {
     in.node_bytes = sizeof(uint2);
     in.prim_bytes = sizeof(float4) + sizeof(uint32_t);
     in.build_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    ++r->scene_gen;  // the camera-relative screen records are remade at the next frame
     r->has_scene = true;
     return RT_OK;
 }
@@ -522,6 +553,22 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     }
     if ((ost = ensure(r, r->counters, words))) return ost;
     if (a.wq_slot_stride) a.wq_slots = reinterpret_cast<uint32_t*>(r->counters.p + kCounterWords);
+    if (r->cfg.mode == RT_MODE_SCENE) {
+        // the camera-relative screen records of this frame's camera origin
+        // (DESIGN.md 5.1): remade on this stream, after the renderer's earlier
+        // frames (order_after_last), when the origin or the scene changed
+        const uint32_t nr = r->info.n_prim_refs + kPrimPad;
+        const float4* before = r->d_prim_cam.p;
+        if ((ost = ensure(r, r->d_prim_cam, nr))) return ost;
+        if (r->d_prim_cam.p != before || r->cam_gen != r->scene_gen ||
+            memcmp(r->cam_o, a.cam.o, sizeof(r->cam_o)) != 0) {
+            hipError_t e = launch_cam_screen(a.sc.prim_sp, nr, a.cam.o, r->d_prim_cam.p, st);
+            if (e != hipSuccess) return hip_fail(r, e, "camera-relative screen records");
+            memcpy(r->cam_o, a.cam.o, sizeof(r->cam_o));
+            r->cam_gen = r->scene_gen;
+        }
+        a.sc.prim_cam = r->d_prim_cam.p;
+    }
     a.counters = r->counters.p;
     RT_HIP(r, hipMemsetAsync(r->counters.p, 0, words * sizeof(unsigned long long), st));
     a.count_work = stats ? 1u : 0u;
@@ -738,6 +785,7 @@ int rt_destroy(rt_renderer* r) {
     r->d_prim_idx.release();
     r->d_spheres.release();
     r->d_albedo.release();
+    r->d_prim_cam.release();
     r->gpu_build.release();
     r->cell_table.release();
     if (r->ev0) (void)hipEventDestroy(r->ev0);
@@ -774,8 +822,15 @@ int rt_resize(rt_renderer* r, uint32_t width, uint32_t height) {
     if (width == 0 || height == 0 || width > 32768 || height > 32768)
         return fail(r, RT_E_INVALID, "rt_resize: width/height out of range");
     int st;
+    // every queued frame that may still write the buffers released below has
+    // finished first, on whichever stream it ran (a caller's, a multi-device
+    // handle's comm and output streams)
+    if (r->multi && (st = multi_wait(r))) return st;
     if ((st = set_device(r))) return st;
     RT_HIP(r, hipStreamSynchronize(r->stream));
+    if (r->pending) RT_HIP(r, hipEventSynchronize(r->done));
+    // a multi-device handle is inconsistent until every device has resized
+    if (r->multi) r->multi->broken = true;
     r->W = width;
     r->H = height;
     r->frames_accum = 0;
@@ -785,8 +840,9 @@ int rt_resize(rt_renderer* r, uint32_t width, uint32_t height) {
     if (r->cfg.flags & RT_FLAG_RADIANCE)
         if ((st = ensure(r, r->rad, (size_t)width * height))) return st;
     rt_resize_intrinsic(width, height, r->K);
-    if (r->multi && (st = multi_synchronize(r))) return st;  // the slabs are re-planned
-    return for_peers(r, [&](rt_renderer* p) { return rt_resize(p, width, height); });
+    if ((st = for_peers(r, [&](rt_renderer* p) { return rt_resize(p, width, height); }))) return st;
+    if (r->multi) r->multi->broken = false;  // the slabs are re-planned at the next frame
+    return RT_OK;
 }
 
 int rt_set_scene(rt_renderer* r, const float* spheres, const uint32_t* albedo, uint32_t n,
@@ -941,15 +997,16 @@ int rt_render(rt_renderer* r, void* dev_rgba8, void* stream, rt_stats* stats) {
     fill_frame_args(r, a);
     a.out8 = dev_rgba8 ? static_cast<uint32_t*>(dev_rgba8) : r->fb.p;
     a.out32 = (r->cfg.flags & RT_FLAG_RADIANCE) ? r->rad.p : nullptr;
-    if (r->multi && (r->cfg.flags & RT_FLAG_RADIANCE))
-        return fail(r, RT_E_STATE, "rt_render: a multi-device handle keeps no radiance buffer");
+    // (a resize whose allocation failed leaves no internal framebuffer)
+    if (!a.out8 || ((r->cfg.flags & RT_FLAG_RADIANCE) && !a.out32))
+        return fail(r, RT_E_STATE, "rt_render: no framebuffer (a resize failed): resize again");
     const auto render_into = [&](hipStream_t hs) -> int {
         return r->multi ? multi_render(r, a.out8, hs, stats) : do_render(r, a, hs, stats);
     };
     if (dev_rgba8 || !r->disp.map) return render_into(static_cast<hipStream_t>(stream));
     // the reference's render(): map the PBO, launch into it, unmap
     // (src/renderer.cu:145-151)
-    hipStream_t hs = stream ? static_cast<hipStream_t>(stream) : r->stream;
+    hipStream_t hs = stream ? static_cast<hipStream_t>(stream) : own_stream(r);
     if ((st = order_after_last(r, hs))) return st;
     void* ptr = nullptr;
     size_t bytes = 0;
@@ -1140,7 +1197,7 @@ int rt_readback(rt_renderer* r, uint8_t* host_rgba8, float* host_rgba32f) {
 
 void* rt_framebuffer(rt_renderer* r) { return r ? r->fb.p : nullptr; }
 
-void* rt_stream(rt_renderer* r) { return r ? static_cast<void*>(r->stream) : nullptr; }
+void* rt_stream(rt_renderer* r) { return r ? static_cast<void*>(own_stream(r)) : nullptr; }
 
 const char* rt_last_error(const rt_renderer* r) {
     if (r) return r->err.c_str();
@@ -1236,7 +1293,7 @@ int multi_plan(rt_renderer* r) {
     MultiState& m = *r->multi;
     if (m.W == r->W && m.H == r->H && m.recv[0]) return RT_OK;
     int st;
-    if ((st = multi_synchronize(r))) return st;
+    if ((st = multi_wait(r))) return st;
     const uint32_t n = static_cast<uint32_t>(m.devs.size()), ts = MultiState::kTs;
     const uint32_t T = ((r->W + ts - 1) / ts) * ((r->H + ts - 1) / ts);
     m.S = (T + n - 1) / n;
@@ -1251,7 +1308,13 @@ int multi_plan(rt_renderer* r) {
             RT_HIP(r, hipSetDevice(m.devs[k]));
             if (m.slab[f][k]) (void)hipFree(m.slab[f][k]);
             m.slab[f][k] = nullptr;
-            RT_HIP(r, hipMalloc(&m.slab[f][k], m.slab_bytes));
+            hipError_t e = m.fault == MultiState::kSlab && k == m.fault_k
+                               ? hipErrorOutOfMemory  // RT_TEST_FAULT=slab:k
+                               : hipMalloc(&m.slab[f][k], m.slab_bytes);
+            if (e != hipSuccess) {
+                m.slab[f][k] = nullptr;
+                return hip_fail(r, e, ("tile slab allocation" + peer_name(m, k)).c_str());
+            }
         }
         RT_HIP(r, hipSetDevice(m.devs[0]));
         if (m.recv[f]) (void)hipFree(m.recv[f]);
@@ -1270,20 +1333,44 @@ int multi_plan(rt_renderer* r) {
     return RT_OK;
 }
 
-int multi_synchronize(rt_renderer* r) {
+// Wait for all of the handle's queued work: every device's render and comm
+// streams, devices[0]'s output stream and the unpacks.
+int multi_wait(rt_renderer* r) {
     MultiState& m = *r->multi;
     for (size_t k = 0; k < m.devs.size(); ++k) {
         RT_HIP(r, hipSetDevice(m.devs[k]));
-        if (m.cs[k]) RT_HIP(r, hipStreamSynchronize(m.cs[k]));
+        if (k < m.cs.size() && m.cs[k]) RT_HIP(r, hipStreamSynchronize(m.cs[k]));
         // (a creation that failed part-way leaves later peers unmade)
         rt_renderer* p = m.peers[k];
         if (!p) continue;
         RT_HIP(r, hipStreamSynchronize(p->stream));
         if (p->pending) RT_HIP(r, hipEventSynchronize(p->done));
     }
+    RT_HIP(r, hipSetDevice(m.devs[0]));
+    if (m.out) RT_HIP(r, hipStreamSynchronize(m.out));
     for (int f = 0; f < MultiState::F; ++f)
         if (m.unpacked[f]) RT_HIP(r, hipEventSynchronize(m.unpacked[f]));
     return RT_OK;
+}
+
+// multi_wait, then every device's check of its last frame (the wave queue's
+// bounded wait flags a frame whose slot was never published): a flagged
+// device's slab was gathered and unpacked incomplete, so the handle reports
+// RT_E_HIP naming that device, as a single-device renderer does for itself.
+int multi_synchronize(rt_renderer* r) {
+    int st;
+    if ((st = multi_wait(r))) return st;
+    MultiState& m = *r->multi;
+    for (size_t k = 0; k < m.peers.size(); ++k) {
+        rt_renderer* p = m.peers[k];
+        if (!p) continue;
+        if ((st = set_device(p)) || (st = check_last_frame(p))) {
+            const std::string msg = p->err + peer_name(m, k);
+            (void)set_device(r);
+            return fail(r, st, msg);
+        }
+    }
+    return set_device(r);
 }
 
 int multi_render(rt_renderer* r, uint32_t* out, hipStream_t hs, rt_stats* stats) {
@@ -1291,8 +1378,10 @@ int multi_render(rt_renderer* r, uint32_t* out, hipStream_t hs, rt_stats* stats)
     int st;
     if (r->cfg.mode == RT_MODE_SCENE && !r->has_scene)
         return fail(r, RT_E_NOSCENE, "RT_MODE_SCENE render without rt_set_scene");
+    if (m.broken)
+        return fail(r, RT_E_STATE, "rt_render: a resize failed on one of the devices: resize again");
     if ((st = multi_plan(r))) return st;
-    if (!hs) hs = r->stream;
+    if (!hs) hs = m.out;
     const uint32_t n = static_cast<uint32_t>(m.devs.size()), ts = MultiState::kTs;
     const int f = static_cast<int>(m.frame % MultiState::F);
     const auto t0 = std::chrono::steady_clock::now();
@@ -1302,12 +1391,18 @@ int multi_render(rt_renderer* r, uint32_t* out, hipStream_t hs, rt_stats* stats)
         rt_renderer* p = m.peers[k];
         RT_HIP(r, hipSetDevice(m.devs[k]));
         if (m.used[f]) RT_HIP(r, hipStreamWaitEvent(p->stream, m.sent[f][k], 0));
+        RT_HIP(r, hipEventRecord(m.started[f][k], p->stream));
         rt_stats sk{};
         st = render_tiles_one(p, m.ids[k].data(), static_cast<uint32_t>(m.ids[k].size()), ts,
                               m.slab[f][k], p->stream, stats ? &sk : nullptr);
         if (st) {
-            r->err = p->err + " (device " + std::to_string(m.devs[k]) + ")";
+            r->err = p->err + peer_name(m, k);
             return st;
+        }
+        if (m.fault == MultiState::kQueue && k == m.fault_k && !stats) {
+            // RT_TEST_FAULT=queue:k: the word the kernel's bounded slot wait
+            // sets (rt_kernels.hip), set after device k's render
+            RT_HIP(r, hipMemsetAsync(p->counters.p + kWaveQueueClaim + 1, 1, 1, p->stream));
         }
         if (stats) {
             sum.primary_rays += sk.primary_rays;
@@ -1436,13 +1531,14 @@ int multi_set_scene_device(rt_renderer* r, uint32_t n, const rt_octree_params* o
 
 void multi_destroy(rt_renderer* r) {
     MultiState* m = r->multi;
-    (void)multi_synchronize(r);
+    (void)multi_wait(r);
     r->multi = nullptr;
     const size_t n = m->devs.size();
     for (size_t k = 0; k < n; ++k) {
         (void)hipSetDevice(m->devs[k]);
         for (int f = 0; f < MultiState::F; ++f) {
             if (k < m->slab[f].size() && m->slab[f][k]) (void)hipFree(m->slab[f][k]);
+            if (k < m->started[f].size() && m->started[f][k]) (void)hipEventDestroy(m->started[f][k]);
             if (k < m->rendered[f].size() && m->rendered[f][k]) (void)hipEventDestroy(m->rendered[f][k]);
             if (k < m->sent[f].size() && m->sent[f][k]) (void)hipEventDestroy(m->sent[f][k]);
         }
@@ -1456,6 +1552,7 @@ void multi_destroy(rt_renderer* r) {
         if (m->recvd[f]) (void)hipEventDestroy(m->recvd[f]);
         if (m->unpacked[f]) (void)hipEventDestroy(m->unpacked[f]);
     }
+    if (m->out) (void)hipStreamDestroy(m->out);
     if (m->out_ready) (void)hipEventDestroy(m->out_ready);
     if (m->d_all_ids) (void)hipFree(m->d_all_ids);
     delete m;
@@ -1487,6 +1584,22 @@ int rt_create_multi(const rt_config* cfg, const int32_t* devices, uint32_t n_dev
     if (transport == RT_TRANSPORT_AUTO) transport = distinct && rccl_api().ok ? RT_TRANSPORT_RCCL : RT_TRANSPORT_PEER;
     if (transport == RT_TRANSPORT_RCCL && !rccl_api().ok)
         return fail(nullptr, RT_E_INVALID, "rt_create_multi: " + rccl_api().why);
+    // the handle renders through packed tile slabs, which carry RGBA8 only
+    if (cfg->flags & RT_FLAG_RADIANCE)
+        return fail(nullptr, RT_E_INVALID,
+                    "rt_create_multi: RT_FLAG_RADIANCE is not supported on a multi-device handle");
+    // test-only fault injection (MultiState::Fault)
+    int fault = MultiState::kNone;
+    uint32_t fault_k = 0;
+    if (const char* fe = getenv("RT_TEST_FAULT")) {
+        const std::string f(fe);
+        const size_t c = f.find(':');
+        const std::string kind = f.substr(0, c);
+        fault_k = c == std::string::npos ? 0u : static_cast<uint32_t>(strtoul(f.c_str() + c + 1, nullptr, 10));
+        fault = kind == "create" ? MultiState::kCreate : kind == "comm" ? MultiState::kComm
+              : kind == "slab" ? MultiState::kSlab : kind == "queue" ? MultiState::kQueue
+              : MultiState::kNone;
+    }
     rt_config c0 = *cfg;
     c0.device = devices[0];
     rt_renderer* r = nullptr;
@@ -1499,12 +1612,15 @@ int rt_create_multi(const rt_config* cfg, const int32_t* devices, uint32_t n_dev
     }
     r->multi = m;
     m->transport = transport;
+    m->fault = fault;
+    m->fault_k = fault_k;
     m->devs.assign(devices, devices + n_devices);
     m->peers.assign(n_devices, nullptr);
     m->peers[0] = r;
     m->cs.assign(n_devices, nullptr);
     for (int f = 0; f < MultiState::F; ++f) {
         m->slab[f].assign(n_devices, nullptr);
+        m->started[f].assign(n_devices, nullptr);
         m->rendered[f].assign(n_devices, nullptr);
         m->sent[f].assign(n_devices, nullptr);
     }
@@ -1516,8 +1632,11 @@ int rt_create_multi(const rt_config* cfg, const int32_t* devices, uint32_t n_dev
     for (uint32_t k = 1; k < n_devices; ++k) {
         rt_config ck = *cfg;
         ck.device = devices[k];
-        if ((st = rt_create(&ck, &m->peers[k]))) {
-            r->err = g_last_error;
+        st = m->fault == MultiState::kCreate && k == m->fault_k
+                 ? fail(nullptr, RT_E_NOMEM, "rt_create: injected failure (RT_TEST_FAULT)")
+                 : rt_create(&ck, &m->peers[k]);
+        if (st) {
+            r->err = "rt_create_multi: " + g_last_error + peer_name(*m, k);
             return bail(st);
         }
     }
@@ -1525,10 +1644,13 @@ int rt_create_multi(const rt_config* cfg, const int32_t* devices, uint32_t n_dev
         hipError_t e = hipSetDevice(devices[k]);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&m->cs[k], hipStreamNonBlocking);
         for (int f = 0; f < MultiState::F && e == hipSuccess; ++f) {
-            e = hipEventCreateWithFlags(&m->rendered[f][k], hipEventDisableTiming);
+            // started / rendered time device k's render (rt_get_multi_timing)
+            e = hipEventCreate(&m->started[f][k]);
+            if (e == hipSuccess) e = hipEventCreate(&m->rendered[f][k]);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&m->sent[f][k], hipEventDisableTiming);
         }
-        if (e != hipSuccess) return bail(hip_fail(r, e, "rt_create_multi: streams/events"));
+        if (e != hipSuccess)
+            return bail(hip_fail(r, e, ("rt_create_multi: streams/events" + peer_name(*m, k)).c_str()));
         if (k && transport == RT_TRANSPORT_PEER && devices[k] != devices[0]) {
             int can = 0;
             if (hipDeviceCanAccessPeer(&can, devices[0], devices[k]) == hipSuccess && can) {
@@ -1540,23 +1662,51 @@ int rt_create_multi(const rt_config* cfg, const int32_t* devices, uint32_t n_dev
     }
     {
         hipError_t e = hipSetDevice(devices[0]);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&m->out, hipStreamNonBlocking);
         for (int f = 0; f < MultiState::F && e == hipSuccess; ++f) {
             e = hipEventCreateWithFlags(&m->recvd[f], hipEventDisableTiming);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&m->unpacked[f], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreate(&m->unpacked[f]);
         }
         if (e == hipSuccess) e = hipEventCreateWithFlags(&m->out_ready, hipEventDisableTiming);
         if (e != hipSuccess) return bail(hip_fail(r, e, "rt_create_multi: events"));
     }
     if (transport == RT_TRANSPORT_RCCL) {
         m->comms.assign(n_devices, nullptr);
-        const ncclResult_t e = rccl_api().CommInitAll(m->comms.data(), static_cast<int>(n_devices), devices);
+        const ncclResult_t e = m->fault == MultiState::kComm
+                                   ? ncclInternalError  // RT_TEST_FAULT=comm
+                                   : rccl_api().CommInitAll(m->comms.data(), static_cast<int>(n_devices), devices);
         if (e != ncclSuccess) {
             m->comms.clear();
-            return bail(nccl_fail(r, e, "ncclCommInitAll"));
+            std::string devs;
+            for (uint32_t k = 0; k < n_devices; ++k) devs += (k ? "," : "") + std::to_string(devices[k]);
+            return bail(nccl_fail(r, e, ("ncclCommInitAll over devices [" + devs + "]").c_str()));
         }
     }
+    // the tile plan and its slabs for the configured size, now: an allocation
+    // failure surfaces here, not at the first frame (a resize re-plans)
+    if ((st = multi_plan(r))) return bail(st);
     (void)hipSetDevice(devices[0]);
     *out = r;
+    return RT_OK;
+}
+
+int rt_get_multi_timing(rt_renderer* r, rt_multi_timing* t) {
+    if (!r || !t) return fail(r, RT_E_INVALID, "rt_get_multi_timing: null argument");
+    if (!r->multi) return fail(r, RT_E_STATE, "rt_get_multi_timing: not a multi-device handle");
+    MultiState& m = *r->multi;
+    if (!m.frame) return fail(r, RT_E_STATE, "rt_get_multi_timing: no frame rendered yet");
+    int st;
+    if ((st = multi_wait(r))) return st;
+    memset(t, 0, sizeof(*t));
+    const int f = static_cast<int>((m.frame - 1) % MultiState::F);
+    t->n_devices = static_cast<uint32_t>(m.devs.size());
+    t->frame = m.frame - 1;
+    for (size_t k = 0; k < m.devs.size(); ++k) {
+        RT_HIP(r, hipSetDevice(m.devs[k]));
+        RT_HIP(r, hipEventElapsedTime(&t->render_ms[k], m.started[f][k], m.rendered[f][k]));
+    }
+    RT_HIP(r, hipSetDevice(m.devs[0]));
+    RT_HIP(r, hipEventElapsedTime(&t->deliver_ms, m.rendered[f][0], m.unpacked[f]));
     return RT_OK;
 }
 

@@ -151,19 +151,17 @@ __device__ __forceinline__ void bs_count(uint32_t* bs, uint32_t i) {
 
 // Nearest root with the perpendicular-distance discriminant, explicit FMAs
 // (13 VALU to the h < 0 test); accepted iff tmin < t < tmax.  Same operations
-// as oracle.c:isect.
-__device__ __forceinline__ bool isect(float o0, float o1, float o2, float d0, float d1, float d2,
-                                      float4 sp, float tmin, float tmax, float& tout,
-                                      uint32_t* bs = nullptr) {
-    const float ocx = o0 - sp.x;
-    const float ocy = o1 - sp.y;
-    const float ocz = o2 - sp.z;
+// as oracle.c:isect.  isect_oc takes o - c already formed (in the same f32
+// operations: the camera-relative records hold it), isect forms it.
+__device__ __forceinline__ bool isect_oc(float ocx, float ocy, float ocz, float d0, float d1,
+                                         float d2, float r, float tmin, float tmax, float& tout,
+                                         uint32_t* bs = nullptr) {
     const float b = fmaf(ocz, d2, fmaf(ocy, d1, ocx * d0));
     const float qx = fmaf(-b, d0, ocx);
     const float qy = fmaf(-b, d1, ocy);
     const float qz = fmaf(-b, d2, ocz);
     const float qq = fmaf(qz, qz, fmaf(qy, qy, qx * qx));
-    const float h = fmaf(sp.w, sp.w, -qq);
+    const float h = fmaf(r, r, -qq);
     if (h < 0.0f) return false;
     RT_BS(kBsSqrt);
     const float sq = sqrtf(h);
@@ -172,6 +170,14 @@ __device__ __forceinline__ bool isect(float o0, float o1, float o2, float d0, fl
     if (!(t > tmin) || !(t < tmax)) return false;
     tout = t;
     return true;
+}
+__device__ __forceinline__ bool isect(float o0, float o1, float o2, float d0, float d1, float d2,
+                                      float4 sp, float tmin, float tmax, float& tout,
+                                      uint32_t* bs = nullptr) {
+    const float ocx = o0 - sp.x;
+    const float ocy = o1 - sp.y;
+    const float ocz = o2 - sp.z;
+    return isect_oc(ocx, ocy, ocz, d0, d1, d2, sp.w, tmin, tmax, tout, bs);
 }
 
 // v_readlane of a float's bits (the builtin is int-typed: a float argument
@@ -182,18 +188,76 @@ __device__ __forceinline__ float readlane_f(float x, uint32_t lane) {
 
 // isect's discriminant h alone (same operations): h < 0 <=> isect rejects
 // the sphere before its square root.
-__device__ __forceinline__ float isect_h(float o0, float o1, float o2, float d0, float d1,
-                                         float d2, float4 sp) {
-    const float ocx = o0 - sp.x;
-    const float ocy = o1 - sp.y;
-    const float ocz = o2 - sp.z;
+__device__ __forceinline__ float isect_h_oc(float ocx, float ocy, float ocz, float d0, float d1,
+                                            float d2, float r) {
     const float b = fmaf(ocz, d2, fmaf(ocy, d1, ocx * d0));
     const float qx = fmaf(-b, d0, ocx);
     const float qy = fmaf(-b, d1, ocy);
     const float qz = fmaf(-b, d2, ocz);
     const float qq = fmaf(qz, qz, fmaf(qy, qy, qx * qx));
-    return fmaf(sp.w, sp.w, -qq);
+    return fmaf(r, r, -qq);
 }
+__device__ __forceinline__ float isect_h(float o0, float o1, float o2, float d0, float d1,
+                                         float d2, float4 sp) {
+    const float ocx = o0 - sp.x;
+    const float ocy = o1 - sp.y;
+    const float ocz = o2 - sp.z;
+    return isect_h_oc(ocx, ocy, ocz, d0, d1, d2, sp.w);
+}
+
+// Camera-relative records (SceneArgs::prim_cam): 0 off; 1 =
+// {o - c, C'} with the slack screen fma(b, b, -C') >= 0 and the exact tests
+// reloading the chunk's spheres; 2 = {o - c, r}, the exact discriminant from
+// the stored o - c (isect's own operations, 10 VALU: no slack, no reload)
+#ifndef RT_CAM_MODE
+#define RT_CAM_MODE 1
+#endif
+constexpr int kCamMode = RT_CAM_MODE;
+
+// The kernel's FrameArgs as memory (the kernarg segment, scalar-cached),
+// behind an opaque pointer: a field read through it is a fresh s_load at that
+// point instead of a value kept live in an SGPR across the walk (the register
+// allocator would spill it into VGPR lanes: v_writelane / v_readlane, VALU
+// work per pixel).  Used for the per-sample camera, shading and output fields.
+typedef __attribute__((address_space(4))) const FrameArgs KernArgs;
+__device__ __forceinline__ KernArgs* kernargs() {
+    KernArgs* p = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
+constexpr uint32_t kSortMaxRounds = 4;  // up to 256 samples per pixel
+constexpr uint32_t kSortMax = 64u * kSortMaxRounds;
+// per wave: per sample a slot {t, sphere} -> {lam | miss g, albedo | miss b}
+// and a kind byte; the tracing order and the list of lit samples (u8 each)
+constexpr uint32_t kSortCellBits = 3;  // jitter cells per axis: 2^3 (8 x 8, Morton order)
+constexpr uint32_t kSortCells = 1u << (2u * kSortCellBits);
+constexpr uint32_t kSortWaveBytes = kSortMax * 8u + 3u * kSortMax + kSortCells * 4u;
+static_assert(kSortWaveBytes % 16u == 0u, "per-wave regions stay float4-aligned");
+
+// rank of this lane among the lanes set in m
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+}
+
+// LDS leaf staging (RT_LDS_LEAF): a per-wave buffer of
+// kLeafBuf spheres after the rest of the workgroup's LDS (pixel sums and
+// stacks, or the sorted path's stacks and per-wave regions).
+#ifndef RT_LDS_LEAF
+#define RT_LDS_LEAF 1
+#endif
+constexpr uint32_t kLeafBuf = 32;  // spheres per wave; a leaf of >= kLeafBuf uses global loads
+// Leaves of fewer spheres read them directly: staging adds an LDS round trip
+// to the first chunk, which a leaf of one or two chunks does not win back.
+// Measured (profiles/r05/ldsmin_ab.log, 3 alternating rounds, against no
+// staging): from 1 / 4 / 6 / 8 spheres C3 +1.0 / -0.7 / -1.7 / +0.2%, C5
+// -6.9 / -7.8 / -7.8 / -5.3%, C5d +4.0 / +2.5 / +2.3 / +2.5%.
+#ifndef RT_LDS_MIN
+#define RT_LDS_MIN 6
+#endif
+constexpr uint32_t kLdsLeafMin = RT_LDS_MIN;
+constexpr size_t kLeafBufBytes = RT_LDS_LEAF ? (kBlockThreads / 64u) * kLeafBuf * sizeof(float4) : 0u;
 
 // Ancestor-stack levels per thread: depths 1..D-1, or K..D-1 with a cell table
 // (a pop above depth K jumps through the table instead).
@@ -207,6 +271,16 @@ __host__ __device__ inline uint32_t stack_levels(const SceneArgs& S, bool no_sta
     if (no_stack && S.tab_k) return 0u;
     const uint32_t sb = S.tab_k ? S.tab_k - 1u : 0u;
     return S.stack_depth > 1u + sb ? S.stack_depth - 1u - sb : 1u;
+}
+
+// First float4 of this wave's LDS leaf buffer (the layout of scene_lds_bytes
+// and sort_lds_bytes).
+__device__ __forceinline__ uint32_t leaf_buf_base(const SceneArgs& S, bool sorted) {
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t head = sorted ? (stack_levels(S, true) * kBlockThreads * 8u +
+                                    (kBlockThreads / 64u) * kSortWaveBytes) / 16u
+                                 : kBlockThreads + stack_levels(S) * kBlockThreads / 2u;
+    return head + wave * kLeafBuf;
 }
 
 // Grid-space octree walk (DESIGN.md "Octree walk"): mirrored origin so every
@@ -227,7 +301,16 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
     const bool kAnyHit = kDynAny ? any_rt : kAnyHitT;
     const uint32_t D = S.max_depth;
     const uint32_t G = 1u << D;
-    const float4* __restrict__ prim_sp = S.prim_sp;
+    // Camera-relative screen: a nearest-hit walk is a primary
+    // ray, whose origin is the frame's camera origin, so its screen reads the
+    // per-frame records {o - c, C'} and tests fma(b, b, -C') >= 0 (4 VALU a
+    // sphere) instead of the full discriminant (13 VALU); the exact tests of a
+    // chunk that passes load the chunk's own sphere records (through a fresh
+    // kernel-argument read: no second array pointer lives in the walk).
+    // Shadow (any-hit) walks start at hit points and keep the full screen.
+    const bool cam = kCamMode != 0 && !kAnyHit;
+    const bool cam_exact = cam && kCamMode == 2;  // records {o - c, r}: the tests use them as they are
+    const float4* __restrict__ prim_sp = cam ? S.prim_cam : S.prim_sp;
     const uint2* __restrict__ nodes = S.nodes;
     const float o[3] = {o0, o1, o2};
     const float d[3] = {d0, d1, d2};
@@ -276,7 +359,8 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         RT_BS(kBsTest);
         if (kAnyHit) RT_BS(kBsTestShadow);
         float th;
-        if (isect(o0, o1, o2, d0, d1, d2, sp, tmin, tmax, th, bs)) {
+        if (cam_exact ? isect_oc(sp.x, sp.y, sp.z, d0, d1, d2, sp.w, tmin, tmax, th, bs)
+                      : isect(o0, o1, o2, d0, d1, d2, sp, tmin, tmax, th, bs)) {
             RT_BS(kBsAccept);
             if (kAnyHit) {
                 tout = th;
@@ -285,18 +369,18 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             if (th < best_t) {
                 best_t = th;
                 best_ref = ref;
-            } else if (th == best_t && S.prim_idx[ref] < S.prim_idx[best_ref]) {
-                best_ref = ref;
+            } else if (th == best_t) {
+                RT_BS(kBsTieLoad);
+                if (S.prim_idx[ref] < S.prim_idx[best_ref]) best_ref = ref;
             }
         }
         return false;
     };
     // Leaf spheres in list order (same order, hence same counters, as the
     // oracle): each lane loads its own, kChunk loads in flight.
-    auto leaf = [&](uint32_t off, uint32_t cnt) -> bool {
-        const float4* __restrict__ ps = prim_sp + off;
-        static_assert(kChunk <= kPrimPad + 1, "leaf loads may run kChunk-1 spheres past a leaf");
-        RT_BS(kBsLeaf);
+    // The chunk loop over one leaf's spheres (offset off, count cnt), each
+    // read as load(k), k counted from the leaf's first reference.
+    auto chunks = [&](auto&& load, uint32_t off, uint32_t cnt) -> bool {
         // cnt >= 1 (a leaf is a non-empty cell; the root leaf is guarded by
         // its caller): a do-while skips the loop-entry test and its branch
         uint32_t j = 0;
@@ -309,13 +393,26 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         };
         do {
             RT_BS(kBsLeafChunk);
+            if (kAnyHit) RT_BS(kBsChunkShadow);
             // kChunk unconditional dwordx4 loads in flight at fixed offsets; a
             // slot past the leaf's end reads the next leaf or the array's
             // kPrimPad tail (in bounds) and is never tested
             float4 sv[kChunk];
+            // slot q >= 1 is fetched only when some lane's leaf still holds
+            // it (RT_SKIP_PAST_END, a wave-uniform branch): a wave-wide load
+            // costs the texture path as much for one lane as for 64, and at
+            // a leaf's odd end the whole wave usually has no slot 1
+            bool fetched[kChunk];
 #pragma unroll
             for (int q = 0; q < kChunk; ++q) {
-                sv[q] = ps[j + q];
+#ifdef RT_SKIP_PAST_END
+                fetched[q] = q == 0 || __any(in_leaf(q));
+                if (fetched[q]) sv[q] = load(j + q);
+                else sv[q] = sv[0];
+#else
+                fetched[q] = true;
+                sv[q] = load(j + q);
+#endif
                 // issue in list order, so the first test waits for its own
                 // sphere only (vmcnt(kChunk-1)), not for the whole chunk
                 __builtin_amdgcn_sched_barrier(0);
@@ -332,13 +429,33 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 // a real sphere record too, and if it passes the screen the
                 // exact tests below still skip it (in_leaf), so it can only
                 // send the chunk down the exact path for nothing
-                const bool pos = !(isect_h(o0, o1, o2, d0, d1, d2, sv[q]) < 0.0f);
-                maybe |= pos;
+                bool pos;
+                if (cam_exact) {
+                    pos = !(isect_h_oc(sv[q].x, sv[q].y, sv[q].z, d0, d1, d2, sv[q].w) < 0.0f);
+                } else if (cam) {
+                    // b exactly as isect computes it ({x,y,z} = o - c in the
+                    // same f32 operations); C' undercuts |o-c|^2 - r^2 by the
+                    // rounding bound, so every sphere isect accepts passes
+                    const float b = fmaf(sv[q].z, d2, fmaf(sv[q].y, d1, sv[q].x * d0));
+                    pos = !(fmaf(b, b, -sv[q].w) < 0.0f);
+                } else {
+                    pos = !(isect_h(o0, o1, o2, d0, d1, d2, sv[q]) < 0.0f);
+                }
+                maybe |= fetched[q] && pos;
             }
             // marked unlikely (it is: most chunks pass no lane): the exact
             // tests are laid out off the fall-through path (C3 -0.6%, C5
             // -0.7%, profiles/r02/branch_hint_ab.log)
+#ifdef RT_BLOCK_STATS
+            if (j + 1u >= cnt) RT_BS(kBsPastEnd);
+#endif
             if (__builtin_expect(__any(maybe), 0)) {
+                if (cam && !cam_exact) {  // the exact tests need the spheres themselves
+                    RT_BS(kBsExactLoad);
+                    const float4* __restrict__ ex = kernargs()->sc.prim_sp + off;
+#pragma unroll
+                    for (int q = 0; q < kChunk; ++q) sv[q] = ex[j + q];
+                }
 #pragma unroll
                 for (int q = 0; q < kChunk; ++q)
                     if (in_leaf(q) && test(sv[q], off + j + q)) return true;
@@ -348,6 +465,37 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             j += kChunk;
         } while (j < cnt);
         return false;
+    };
+    auto leaf = [&](uint32_t off, uint32_t cnt) -> bool {
+        static_assert(kChunk <= kPrimPad + 1, "leaf loads may run kChunk-1 spheres past a leaf");
+        RT_BS(kBsLeaf);
+#if RT_LDS_LEAF
+        // A leaf the whole wave is at (the common case: one pixel's samples
+        // walk together): its spheres cross the texture path ONCE, each
+        // active lane fetching one into the wave's LDS leaf buffer, and the
+        // chunks read them back by LDS broadcast (every lane the same
+        // address): one dwordx4 texture instruction per leaf visit instead
+        // of two per chunk (DESIGN.md 5.1 "LDS leaf staging").  The buffer
+        // is a typed LDS array, never a generic pointer (round 3's flat
+        // loads).  A slot past the leaf's end holds a stale sphere, which
+        // the exact tests skip as before.
+        const uint32_t off_u = __builtin_amdgcn_readfirstlane(off);
+        const uint32_t cnt_u = __builtin_amdgcn_readfirstlane(cnt);
+        if (cnt_u >= kLdsLeafMin && cnt_u < kLeafBuf && __all(off == off_u)) {
+            RT_BS(kBsLdsLeaf);
+            extern __shared__ __attribute__((aligned(16))) float4 lds_leaf[];
+            const uint32_t lb = leaf_buf_base(S, kNoStack);
+            const float4* __restrict__ pu = prim_sp + off_u;
+            const uint64_t act = __ballot(1);
+            const uint32_t na = static_cast<uint32_t>(__popcll(act));
+            for (uint32_t k = lane_rank(act); k < cnt_u; k += na) lds_leaf[lb + k] = pu[k];
+            // (a wave's LDS operations complete in order: the reads below see
+            // the writes, and the compiler keeps them in order: same array)
+            return chunks([&](uint32_t k) { return lds_leaf[lb + k]; }, off_u, cnt_u);
+        }
+#endif
+        const float4* __restrict__ ps = prim_sp + off;
+        return chunks([&](uint32_t k) { return ps[k]; }, off, cnt);
     };
 
     if (S.root_is_leaf) {
@@ -389,6 +537,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 // descent's child choices), then the cell's table entry
                 while (depth < K) {
                     RT_BS(kBsJumpDescend);
+                    if (kAnyHit) RT_BS(kBsJumpDescendShadow);
                     const uint32_t half = size >> 1;
                     l0 += plane(0, l0 + half) <= t ? half : 0u;
                     l1 += plane(1, l1 + half) <= t ? half : 0u;
@@ -437,6 +586,10 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 if (have) {
                     const uint32_t slot = node.x + __builtin_popcount(valid & ((1u << child) - 1u));
                     rec = nodes[slot];
+#ifdef RT_BLOCK_STATS
+                    if (depth > from) RT_BS(kBsNodeRead);
+                    else RT_BS(kBsNodeReread);
+#endif
                     // records down to a re-entered ancestor are the oracle's
                     // stack pops, not reads
                     if (kStats && depth > from) n_nodes += 1;
@@ -513,6 +666,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         if (any_hit) return true;
     }
     if (!kAnyHit && best_ref != kNoHit) {
+        RT_BS(kBsHitIdx);
         tout = best_t;
         iout = S.prim_idx[best_ref];
         return true;
@@ -573,18 +727,6 @@ __device__ __forceinline__ void flush_counters(const FrameArgs& a, uint32_t prim
     }
 }
 
-// The kernel's FrameArgs as memory (the kernarg segment, scalar-cached),
-// behind an opaque pointer: a field read through it is a fresh s_load at that
-// point instead of a value kept live in an SGPR across the walk (the register
-// allocator would spill it into VGPR lanes: v_writelane / v_readlane, VALU
-// work per pixel).  Used for the per-sample camera, shading and output fields.
-typedef __attribute__((address_space(4))) const FrameArgs KernArgs;
-__device__ __forceinline__ KernArgs* kernargs() {
-    KernArgs* p = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(p));
-    return p;
-}
-
 // Unified lane path: one walk instance run twice (primary, then the shadow ray
 // of the lanes that need one), so the register allocator sees one walk.
 template <int kChunk, bool kStats>
@@ -608,9 +750,13 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
         get_ray(cam, u, v, d0, d1, d2);
     }
     const float miss_g = sat(d1), miss_b = sat(d2);
-    bool active = valid, any = false, hit0 = false;
+    bool active = valid, hit0 = false;
     float lam = 0.0f;
     uint32_t al = 0;
+    // the primary and the shadow walk as two instances (the phase loop was
+    // always unrolled into two copies; written out so that the primary one
+    // keeps the camera-relative screen, a compile-time choice)
+#pragma unroll
     for (int phase = 0; phase < 2; ++phase) {
         float t = 0.0f;
         uint32_t idx = 0;
@@ -618,15 +764,22 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
         if (active) {
             RT_BS(kBsPhase);
             if (phase) RT_BS(kBsPhaseShadow);
-            hit = walk<false, kChunk, true, kStats>(S, r0, r1, r2, d0, d1, d2, 0.0f, INFINITY, t,
-                                                    idx, n_nodes, n_prims,
-                                                    static_cast<uint2*>(stk), any, bs);
+            if (phase == 0)
+                hit = walk<false, kChunk, false, kStats>(S, r0, r1, r2, d0, d1, d2, 0.0f, INFINITY, t,
+                                                         idx, n_nodes, n_prims,
+                                                         static_cast<uint2*>(stk), false, bs);
+            else
+                hit = walk<true, kChunk, false, kStats>(S, r0, r1, r2, d0, d1, d2, 0.0f, INFINITY, t,
+                                                        idx, n_nodes, n_prims,
+                                                        static_cast<uint2*>(stk), true, bs);
         }
         if (phase == 0) {
             hit0 = active && hit;
             bool want_shadow = false;
             KernArgs* kb = kernargs();
             if (hit0) {
+                RT_BS(kBsShadeLoad);  // the sphere record
+                RT_BS(kBsShadeLoad);  // the albedo
                 const float4 sp = kb->sc.spheres[idx];
                 const float p0 = r0 + t * d0;
                 const float p1 = r1 + t * d1;
@@ -647,7 +800,6 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
                 d2 = kb->L[2];
             }
             active = want_shadow;
-            any = true;
             n_shadow += static_cast<uint32_t>(__popcll(__ballot(active)));  // wave-uniform
             if (!__any(active)) break;
         } else if (active && hit) {
@@ -754,20 +906,6 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
 // predicts 11% fewer primary and 13% fewer shadow trips on C5.
 // ---------------------------------------------------------------------------
 
-constexpr uint32_t kSortMaxRounds = 4;  // up to 256 samples per pixel
-constexpr uint32_t kSortMax = 64u * kSortMaxRounds;
-// per wave: per sample a slot {t, sphere} -> {lam | miss g, albedo | miss b}
-// and a kind byte; the tracing order and the list of lit samples (u8 each)
-constexpr uint32_t kSortCellBits = 3;  // jitter cells per axis: 2^3 (8 x 8, Morton order)
-constexpr uint32_t kSortCells = 1u << (2u * kSortCellBits);
-constexpr uint32_t kSortWaveBytes = kSortMax * 8u + 3u * kSortMax + kSortCells * 4u;
-static_assert(kSortWaveBytes % 16u == 0u, "per-wave regions stay float4-aligned");
-
-// rank of this lane among the lanes set in m
-__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
-                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
-}
 
 // Morton cell of sample sg's jitter on a 2^kSortCellBits grid per axis (the
 // top bits of each hash are its u01 in those steps): the top two bits are
@@ -800,9 +938,11 @@ __device__ __forceinline__ void sample_dir(uint32_t x, uint32_t y, uint32_t hp, 
 struct HitShade {
     float p0, p1, p2, n0, n1, n2, ndl;
 };
-__device__ __forceinline__ HitShade hit_shade(float d0, float d1, float d2, float t, uint32_t idx) {
+__device__ __forceinline__ HitShade hit_shade(float d0, float d1, float d2, float t, uint32_t idx,
+                                              uint32_t* bs = nullptr) {
     KernArgs* kb = kernargs();
     const float4 sp = kb->sc.spheres[idx];
+    RT_BS(kBsShadeLoad);
     HitShade h;
     h.p0 = kb->cam.o[0] + t * d0;
     h.p1 = kb->cam.o[1] + t * d1;
@@ -897,12 +1037,13 @@ __device__ __forceinline__ void shade_pixel_sorted(const FrameArgs& a, float* wl
             uint2 sv = make_uint2(__float_as_uint(sat(d1)), __float_as_uint(sat(d2)));
             uint8_t kd = 0;
             if (hit) {
-                const HitShade h = hit_shade(d0, d1, d2, t, idx);
+                const HitShade h = hit_shade(d0, d1, d2, t, idx, bs);
                 is_lit = h.ndl > 0.0f && kernargs()->shadows;
                 if (is_lit) {
                     sv = make_uint2(__float_as_uint(t), idx);
                     kd = 2;
                 } else {
+                    RT_BS(kBsShadeLoad);
                     sv = make_uint2(__float_as_uint(h.ndl > 0.0f ? h.ndl : 0.0f),
                                     kernargs()->sc.albedo[idx]);
                     kd = 1;
@@ -928,7 +1069,7 @@ __device__ __forceinline__ void shade_pixel_sorted(const FrameArgs& a, float* wl
             sample_dir(x, y, hp, s_base + sl, d0, d1, d2);
             const uint2 sv = slot[sl];
             idx = sv.y;
-            const HitShade h = hit_shade(d0, d1, d2, __uint_as_float(sv.x), idx);
+            const HitShade h = hit_shade(d0, d1, d2, __uint_as_float(sv.x), idx, bs);
             lam = h.ndl > 0.0f ? h.ndl : 0.0f;
             o0 = h.p0 + h.n0 * kShadowEps;
             o1 = h.p1 + h.n1 * kShadowEps;
@@ -946,6 +1087,7 @@ __device__ __forceinline__ void shade_pixel_sorted(const FrameArgs& a, float* wl
                                                           static_cast<uint2*>(stk), true, bs);
         }
         if (has) {
+            RT_BS(kBsShadeLoad);
             slot[sl] = make_uint2(__float_as_uint(occ ? 0.0f : lam), kernargs()->sc.albedo[idx]);
             kind[sl] = 1;
         }
@@ -1277,6 +1419,34 @@ __global__ void __launch_bounds__(kBlockThreads, 8) __attribute__((amdgpu_num_sg
     scene_body<kTiles, 2, false, kProg, true, kSort>(a);
 }
 
+// Camera-relative screen records of every leaf reference (and the kPrimPad
+// tail) for camera origin o (SceneArgs::prim_cam):
+// {o - c in f32, exactly isect's oc}, and C' = |o - c|^2 - r^2 minus the
+// slack, computed in f64 and rounded toward -inf, so C' <= the bound the
+// screen's soundness needs.  One thread per reference: 16 B read, 16 B written.
+__global__ void __launch_bounds__(kBlockThreads)
+    cam_screen_kernel(const float4* __restrict__ prim_sp, uint32_t n, float ox, float oy, float oz,
+                      float4* __restrict__ out) {
+    const uint32_t i = blockIdx.x * kBlockThreads + threadIdx.x;
+    if (i >= n) return;
+    const float4 c = prim_sp[i];
+    const float x = ox - c.x, y = oy - c.y, z = oz - c.z;
+    const double oo = static_cast<double>(x) * x + static_cast<double>(y) * y + static_cast<double>(z) * z;
+    const double rr = static_cast<double>(c.w) * c.w;
+    const double u = 1.0 / 16777216.0;  // 2^-24, the f32 unit roundoff
+    const double cd = oo - rr - (kScreenSlackOc * u) * oo - (kScreenSlackR * u) * rr;
+    out[i] = make_float4(x, y, z, kCamMode == 2 ? c.w : __double2float_rd(cd));
+}
+
+hipError_t launch_cam_screen(const float4* prim_sp, uint32_t n, const float o[3], float4* out,
+                             hipStream_t st) {
+    if (n) {
+        hipLaunchKernelGGL(cam_screen_kernel, dim3((n + kBlockThreads - 1) / kBlockThreads),
+                           dim3(kBlockThreads), 0, st, prim_sp, n, o[0], o[1], o[2], out);
+    }
+    return hipGetLastError();
+}
+
 __global__ void __launch_bounds__(kBlockThreads)
     unpack_kernel(const uint32_t* __restrict__ packed, const uint32_t* __restrict__ tiles,
                   uint32_t n_tiles, uint32_t ts, uint32_t tiles_x, uint32_t W, uint32_t H,
@@ -1312,7 +1482,7 @@ hipError_t launch_compat(const FrameArgs& a, hipStream_t st) {
 size_t scene_lds_bytes(const FrameArgs& a) {
     const size_t colours = kBlockThreads * sizeof(float4);  // pixel sums
     const uint32_t levels = stack_levels(a.sc);
-    return colours + static_cast<size_t>(levels) * kBlockThreads * sizeof(uint2);
+    return colours + static_cast<size_t>(levels) * kBlockThreads * sizeof(uint2) + kLeafBufBytes;
 }
 
 // Resident workgroups on the device for a kernel at a given LDS size.  The
@@ -1439,7 +1609,7 @@ static uint32_t env_u32(const char* name, uint32_t dflt) {
 }
 size_t sort_lds_bytes(const FrameArgs& a) {
     return static_cast<size_t>(stack_levels(a.sc, true)) * kBlockThreads * sizeof(uint2) +
-           (kBlockThreads / 64) * kSortWaveBytes;
+           (kBlockThreads / 64) * kSortWaveBytes + kLeafBufBytes;
 }
 static bool sorted_rounds(const FrameArgs& a) {
     static const uint32_t on = env_u32("RT_SORT", 1u);

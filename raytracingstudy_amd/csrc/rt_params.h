@@ -88,6 +88,19 @@ enum BlockStat : uint32_t {
     kBsIterShadow,    // walk loop trips of shadow (any-hit) walks
     kBsTestShadow,    // sphere tests of shadow walks
     kBsPhaseShadow,   // shadow phases run by the wave
+    // vector-memory loads by class (round 5; one wave
+    // execution = one load instruction): sphere pairs are 2 x kBsLeafChunk and
+    // table entries kBsJump; these add the rest
+    kBsNodeRead,      // child record reads of a descent (oracle-counted)
+    kBsNodeReread,    // child record re-reads below a re-entered ancestor (not counted by the oracle)
+    kBsExactLoad,     // chunks whose camera-relative screen passed: 2 sphere loads for the exact tests
+    kBsPastEnd,       // chunks whose slot 1 lies past the leaf's end (lanes: how many)
+    kBsTieLoad,       // exact-t ties: 2 prim_idx loads
+    kBsHitIdx,        // nearest walks ending on a hit: 1 prim_idx load
+    kBsShadeLoad,     // shading reads of a hit's sphere record / albedo (1 load each)
+    kBsChunkShadow,   // leaf chunk trips of shadow (any-hit) walks
+    kBsJumpDescendShadow,  // jump mid-plane steps of shadow walks
+    kBsLdsLeaf,       // leaf visits staged through the wave's LDS buffer (RT_LDS_LEAF)
     kBlockStats
 };
 
@@ -172,7 +185,20 @@ struct SceneArgs {
     const uint2* tab;        // depth-tab_k cell table, or null (cell_table.hip)
     uint32_t tab_k;          // 0: no table
     uint32_t stack_depth;    // deepest leaf (sizes the per-lane ancestor stack)
+    // Camera-relative screen records (DESIGN.md 5.1 "Camera-relative screen"):
+    // per leaf reference {o - c (f32, as isect computes it), C'} with
+    // C' <= |o - c|^2 - r^2 - slack, for the camera origin o of the frame
+    // (cam_screen_kernel, refreshed when the origin or the scene changes).
+    // Primary rays screen a sphere by fma(b, b, -C') >= 0 with b = (o - c).d.
+    const float4* prim_cam;
 };
+
+// Slack of the camera-relative screen, in units of 2^-24: the
+// screen may only pass MORE spheres than the exact test, so C' undercuts
+// |o - c|^2 - r^2 by the bound on the two forms' rounding difference
+// (13 u |o - c|^2 + 5 u r^2 derived there; 16 and 8 kept).
+constexpr double kScreenSlackOc = 16.0;
+constexpr double kScreenSlackR = 8.0;
 
 struct FrameArgs {
     CamArgs cam;

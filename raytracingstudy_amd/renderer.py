@@ -285,6 +285,14 @@ class KernelRenderer:
         check(self._lib.rt_get_multi_info(self._h, ctypes.byref(info)), self._h)
         return info.as_dict()
 
+    def multi_timing(self) -> dict:
+        """rt_get_multi_timing: per-device render ms of the last frame (HIP
+        events on each device's render stream) and devices[0]'s delivery ms
+        (its own tiles' end -> the frame unpacked).  Waits for the handle."""
+        t = _lib.RtMultiTiming()
+        check(self._lib.rt_get_multi_timing(self._h, ctypes.byref(t)), self._h)
+        return t.as_dict()
+
     def camera(self):
         pose = np.zeros(16, np.float32)
         K = np.zeros(9, np.float32)

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _lib.load().rt_abi_version() == 3
+    assert _lib.load().rt_abi_version() == 4
 
 
 def test_library_has_gfx950_code_object():

@@ -155,6 +155,144 @@ def test_progressive_and_display_on_multi(gpu, oracle):
         assert np.array_equal(buf.cpu().numpy().reshape(h, w, 4), want)
 
 
+def _free_bytes():
+    import torch
+    torch.cuda.synchronize()
+    return torch.cuda.mem_get_info(0)[0]
+
+
+def _create_multi(devs, transport, w=1920, h=1080, flags=0):
+    lib = _lib.load()
+    cfg = _lib.RtConfig()
+    lib.rt_config_default(ctypes.byref(cfg))
+    cfg.mode = _lib.RT_MODE_SCENE
+    cfg.width, cfg.height, cfg.spp = w, h, 4
+    cfg.flags = flags
+    h_ = ctypes.c_void_p()
+    arr = (ctypes.c_int32 * len(devs))(*devs)
+    st = lib.rt_create_multi(ctypes.byref(cfg), arr, len(devs), transport, ctypes.byref(h_))
+    return st, h_
+
+
+@pytest.mark.parametrize("fault,devs,transport,code,names", [
+    ("create:2", [0, 0, 0], _lib.RT_TRANSPORT_PEER, _lib.RT_E_NOMEM, b"peer 2"),
+    ("create:1", [0, 0], _lib.RT_TRANSPORT_PEER, _lib.RT_E_NOMEM, b"peer 1"),
+    ("slab:1", [0, 0, 0], _lib.RT_TRANSPORT_PEER, _lib.RT_E_HIP, b"peer 1"),
+    ("slab:0", [0], _lib.RT_TRANSPORT_RCCL, _lib.RT_E_HIP, b"peer 0"),
+    ("comm", [0], _lib.RT_TRANSPORT_RCCL, _lib.RT_E_HIP, b"devices [0]"),
+])
+def test_multi_create_fault_injection(gpu, monkeypatch, fault, devs, transport, code, names):
+    """a failure of peer k's renderer, of ncclCommInitAll
+    or of a slab allocation fails rt_create_multi with the error, names the
+    device in rt_last_error(NULL), returns no handle, and frees what the
+    partial creation made (the b69acc2 path: peers after k never made).
+    Repeated 6 times at 1080p (each attempt allocates tens of MB) with the
+    device's free memory checked before and after."""
+    lib = _lib.load()
+    monkeypatch.setenv("RT_TEST_FAULT", fault)
+    st, h = _create_multi(devs, transport)  # warm up allocator / RCCL state once
+    assert st == code and not h.value
+    before = _free_bytes()
+    for _ in range(6):
+        st, h = _create_multi(devs, transport)
+        assert st == code, lib.rt_last_error(None)
+        assert not h.value
+        msg = lib.rt_last_error(None)
+        assert names in msg and b"device 0" in msg or fault == "comm", msg
+    assert before - _free_bytes() < 32 << 20, "device memory leaked by failed creations"
+    monkeypatch.delenv("RT_TEST_FAULT")
+    st, h = _create_multi(devs, transport)  # no fault: the same creation succeeds
+    assert st == _lib.RT_OK, lib.rt_last_error(None)
+    lib.rt_destroy(h)
+
+
+def test_multi_peer_queue_error_is_reported(gpu, monkeypatch):
+    """a peer whose frame flags its wave-queue error (a
+    slot never published, so its slab is incomplete) makes rt_synchronize and
+    rt_readback return RT_E_HIP naming that peer, as a single-device renderer
+    does for itself; the next clean frame synchronizes without error."""
+    monkeypatch.setenv("RT_TEST_FAULT", "queue:1")
+    w, h, spp = 160, 96, 4
+    sp, al = rt.generate_spheres(1000, rt.SEED)
+    with _scene_renderer(w, h, spp, sp, al, devices=[0, 0, 0]) as r:
+        r.render()
+        with pytest.raises(_lib.RtError) as e:
+            r.synchronize()
+        assert e.value.code == _lib.RT_E_HIP and "peer 1" in str(e.value), str(e.value)
+        r.render()
+        with pytest.raises(_lib.RtError) as e:
+            r.readback()
+        assert e.value.code == _lib.RT_E_HIP and "peer 1" in str(e.value)
+        st = r.render(stats=True)  # stats frames are not faulted: clean
+        assert st.primary_rays == w * h * spp
+        r.synchronize()
+
+
+def test_multi_default_stream_and_timing(gpu):
+    """with no stream the handle uses its own output stream
+    on devices[0], not devices[0]'s render stream; rt_get_multi_timing gives
+    every device's render time of the last frame and devices[0]'s delivery."""
+    w, h, spp = 320, 200, 8
+    sp, al = rt.generate_spheres(2000, rt.SEED)
+    ref, _ = _whole(w, h, spp, sp, al)
+    with _scene_renderer(w, h, spp, sp, al, devices=[0, 0]) as r:
+        with pytest.raises(_lib.RtError) as e:
+            r.multi_timing()  # no frame yet
+        assert e.value.code == _lib.RT_E_STATE
+        for _ in range(3):
+            r.render()
+        t = r.multi_timing()
+        assert t["n_devices"] == 2 and t["frame"] == 2
+        assert all(x > 0 for x in t["render_ms"]) and t["deliver_ms"] > 0
+        assert np.array_equal(r.readback(), ref)
+        out = r.stream_ptr()
+        assert out and out != 0
+    with _scene_renderer(w, h, spp, sp, al) as r1:
+        with pytest.raises(_lib.RtError) as e:
+            r1.multi_timing()
+        assert e.value.code == _lib.RT_E_STATE
+
+
+def test_multi_refuses_radiance_and_resize_keeps_frames(gpu):
+    """RT_FLAG_RADIANCE is refused at creation; a resize
+    waits for in-flight frames on the caller's stream before it frees them."""
+    import torch
+    st, h = _create_multi([0, 0], _lib.RT_TRANSPORT_PEER, w=64, h=64, flags=_lib.RT_FLAG_RADIANCE)
+    assert st == _lib.RT_E_INVALID and b"RADIANCE" in _lib.load().rt_last_error(None)
+    w, h, spp = 256, 160, 16
+    sp, al = rt.generate_spheres(3000, rt.SEED)
+    s = torch.cuda.Stream()
+    with _scene_renderer(w, h, spp, sp, al, devices=[0, 0]) as r:
+        for _ in range(2):
+            r.render(None, s.cuda_stream)
+        r.resize(96, 64)  # frames queued on s are still running
+        r.setPosition(scene_pose())
+        r.render()
+        ref, _ = _whole(96, 64, spp, sp, al)
+        assert np.array_equal(r.readback(), ref)
+
+
+def test_bench_native_one_device(gpu):
+    """`bench.py --gpus 1 --native` drives the C-ABI's
+    multi-device handle as a 1-device RCCL communicator; its frame equals one
+    renderer's whole frame and the line names the transport and device times."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "1", "--native",
+                        "--config", "c2", "--steps", "5", "--warmup", "2"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    c = line["config"]
+    assert line["n_gpus"] == 1 and c["transport"] == "rccl" and c["tiles_frame_check"] is True
+    assert c["devices_seen"] >= 1 and len(c["device_render_ms"]) == 1
+    assert line["value"] > 0 and line["roofline"]["frac"] > 0
+
+
 def test_multi_refusals(gpu):
     lib = _lib.load()
     cfg = _lib.RtConfig()

@@ -12,6 +12,7 @@ import sys
 
 def main(path):
     runs = collections.defaultdict(list)
+    sigs = collections.defaultdict(set)  # (cfg) -> {(image hash, counters)} over every library
     libs = []
     for line in open(path):
         if line.startswith("#") or not line.strip():
@@ -21,11 +22,16 @@ def main(path):
             libs.append(lib)
         for v in json.loads(js).values():
             runs[(cfg, lib)].append(v["ms_median"])
+            if "image_sha1" in v:
+                sigs[cfg].add((v["image_sha1"], tuple(v.get("counters", ()))))
     for cfg in sorted({c for c, _ in runs}):
         base = statistics.median(runs[(cfg, libs[0])])
         for lib in libs:
             m = statistics.median(runs[(cfg, lib)])
             print(f"{cfg:4s} {lib:10s} {m:8.3f} ms  {100 * (m / base - 1):+5.1f}%  {runs[(cfg, lib)]}")
+        if sigs[cfg]:
+            print(f"{cfg:4s} images and counters {'IDENTICAL' if len(sigs[cfg]) == 1 else 'DIFFER'} "
+                  f"across the libraries ({len(sigs[cfg])} distinct)")
 
 
 if __name__ == "__main__":

@@ -22,7 +22,9 @@ sys.path.insert(0, ROOT)
 
 NAMES = ["iter", "jump", "jump_descend", "descend", "internal", "leaf", "leaf_chunk", "test",
          "sqrt", "accept", "exit", "pop", "walk", "phase", "iter_shadow", "test_shadow",
-         "phase_shadow"]
+         "phase_shadow", "node_read", "node_reread", "exact_load", "past_end", "tie_load", "hit_idx",
+         "shade_load", "chunk_shadow", "jump_descend_shadow",
+         "lds_leaf"]
 
 
 def main():

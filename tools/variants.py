@@ -82,6 +82,10 @@ def main():
                       "nodes_per_ray": round(st.nodes_visited / rays, 2),
                       "prims_per_ray": round(st.prims_tested / rays, 2),
                       "cell_table_depth": rs[v].cell_table_depth,
+                      # across libraries (tools/ab_libs.sh): equal images, equal hashes
+                      "image_sha1": __import__("hashlib").sha1(img.tobytes()).hexdigest()[:12],
+                      "counters": [int(st.primary_rays), int(st.shadow_rays), int(st.nodes_visited),
+                                   int(st.prims_tested)],
                       "image_equal_to_v%s" % variants[0]: bool(np.array_equal(img, ref))}
             rs[v].close()
         out[f"{name} spp{spp}"] = res
