@@ -138,6 +138,8 @@ struct rt_renderer {
     uint32_t n_spheres = 0;
     std::vector<float> spheres;
     bool host_copy = false;
+    // test only: RT_TEST_CLAIM_DELAY at rt_create (FrameArgs::wq_claim_delay)
+    uint32_t test_claim_delay = 0;
     rt_octree_params oct;
     bool has_scene = false;
     GpuOctreeBuilder gpu_build;
@@ -268,6 +270,7 @@ void fill_frame_args(rt_renderer* r, FrameArgs& a) {
     }
     a.counters = r->counters.p;
     a.sc.opt = (r->cfg.flags >> RT_FLAG_OPT_SHIFT) & 0xFFu;
+    a.wq_claim_delay = r->test_claim_delay;
     const uint32_t v = (r->cfg.flags >> RT_FLAG_VARIANT_SHIFT) & 0xFu;
     // default: multi-sample frames are scheduled per wave over per-XCD queues
     // (variant 13: C5 -15%, equal on C3, better on multi-GPU shares); 1-spp
@@ -729,6 +732,8 @@ int rt_create(const rt_config* cfg, rt_renderer** out) {
     r->device = dev;
     r->W = cfg->width;
     r->H = cfg->height;
+    if (const char* cd = getenv("RT_TEST_CLAIM_DELAY"))  // test only (tests/test_gpu_variants.py)
+        r->test_claim_delay = static_cast<uint32_t>(std::min(100000ul, strtoul(cd, nullptr, 10)));
     // src/renderer.cu:87-89: K0 = mat3(1000,0,640, 0,1000,340, 0,0,1), pose = mat4(1)
     const float K0[9] = {1000.f, 0.f, 640.f, 0.f, 1000.f, 340.f, 0.f, 0.f, 1.f};
     memcpy(r->K, K0, sizeof(K0));

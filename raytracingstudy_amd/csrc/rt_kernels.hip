@@ -1238,19 +1238,37 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
             if ((threadIdx.x & 63u) == 0) t = static_cast<uint32_t>(atomicAdd(head, 1ull));
             const uint32_t u0 = __builtin_amdgcn_readfirstlane(t) * chunk;
             const uint32_t s = u0 >> ks, w0 = u0 & ((1u << ks) - 1u);
-            if ((threadIdx.x & 63u) == 0 && (u0 == 0u || (w0 <= half && half < w0 + chunk))) {
-                const uint32_t slot = u0 == 0u ? 0u : s + 1u;
+            const bool lead = (threadIdx.x & 63u) == 0;
+            // One claim per slot, in slot order: ticket 0 claims slot 0, and
+            // the ticket holding slot s's middle unit claims slot s + 1 only
+            // AFTER it has seen slot s published.  An XCD's claims are thus
+            // taken from the counter in slot order, so a slot past the last
+            // superblock (kSlotNone) is never followed by a real one.  Claimed
+            // in ticket order instead (before round 5), two claims could
+            // cross at the counter's end: slot s got kSlotNone and slot s + 1
+            // the last block, and when every wave of the XCD had drawn one of
+            // slot s's tickets and exited, no wave was left for that block
+            // (an image block left unwritten; test_gpu_variants.py
+            // test_wave_queue_claims_in_slot_order).  The claim's atomic is
+            // issued after the load that saw slot s published returned, and
+            // that value was stored after slot s's own claim returned: both
+            // returning atomics are performed at the one counter, in that order.
+            if (lead && u0 == 0u) {
+                // (test only: hold XCD 0's first claim back until the other
+                // claims of its first slots would have been taken)
+                if (q == 0u)
+                    for (uint32_t d = kernargs()->wq_claim_delay; d; --d) __builtin_amdgcn_s_sleep(127);
                 const uint32_t g = static_cast<uint32_t>(atomicAdd(claims, 1ull));
-                if (slot < a.wq_slot_stride)
-                    __hip_atomic_store(slots + slot, g < n1 ? g + 1u : kSlotNone, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(slots, g < n1 ? g + 1u : kSlotNone, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             }
+            uint32_t e = kSlotNone;
             if (s != cached_s) {  // resolve the slot's superblock or block (published, or soon)
-                uint32_t e = kSlotNone;
-                if ((threadIdx.x & 63u) == 0 && s < a.wq_slot_stride) {
-                    // the claimer holds a ticket already and publishes before it
-                    // waits on anything; the cap (~1 s) only turns a broken
-                    // invariant into a flagged, visibly wrong frame, not a hang
+                if (lead && s < a.wq_slot_stride) {
+                    // its claimer holds a ticket of slot s - 1 (or ticket 0),
+                    // which waits on nothing later than slot s - 1; the cap
+                    // (~1 s) only turns a broken invariant into a flagged,
+                    // visibly wrong frame, not a hang
                     for (uint32_t spin = 0;; ++spin) {
                         e = __hip_atomic_load(slots + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         if (e != 0u) break;
@@ -1263,6 +1281,14 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
                     }
                 }
                 e = __builtin_amdgcn_readfirstlane(e);
+            }
+            if (lead && u0 != 0u && w0 <= half && half < w0 + chunk) {
+                const uint32_t g = static_cast<uint32_t>(atomicAdd(claims, 1ull));
+                if (s + 1u < a.wq_slot_stride)
+                    __hip_atomic_store(slots + s + 1u, g < n1 ? g + 1u : kSlotNone, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (s != cached_s) {
 #ifdef RT_TIMELINE
                 if (e == kSlotNone && !tl_empty) tl_empty = wall_clock64();
 #endif

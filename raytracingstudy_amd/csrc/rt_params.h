@@ -234,6 +234,8 @@ struct FrameArgs {
     uint32_t* wq_slots;        // two-level wave queue: per XCD, the superblock of each slot + 1
     uint32_t wq_slot_stride;   //   (0 = not claimed yet, kSlotNone = none left); zeroed per frame
     uint32_t wq_slot_shift;    //   slot = 2^shift wave tiles: 12 a superblock, 6 one 8x8 block
+    uint32_t wq_claim_delay;   // test only (RT_TEST_CLAIM_DELAY): XCD 0's ticket-0 wave sleeps
+                               //   this many s_sleep 127 before claiming slot 0; 0 in product
 #ifdef RT_TIMELINE
     unsigned long long* timeline;  // diagnostic build: 4 words per wave
 #endif

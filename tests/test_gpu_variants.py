@@ -71,6 +71,53 @@ def test_variants_independent_of_pad(gpu, oracle, case):
     assert not bad, bad
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [(9, 48, 40, 16, 7), (20000, 128, 96, 2, 12)],
+                         ids=lambda c: "n%d_%dx%d_s%d_d%d" % c)
+@pytest.mark.parametrize("delay", [0, 30])
+def test_wave_queue_claims_in_slot_order(gpu, oracle, case, delay, monkeypatch):
+    """Every frame writes every pixel, even when XCD 0's first slot claim is
+    held back (RT_TEST_CLAIM_DELAY: ~100 us of s_sleep before it) until the
+    other claims of its first slots have been taken.  These frames hold 9
+    and 6 blocks for 8 XCDs, so the level-1 counter runs out inside the
+    first slots.  Claimed in ticket order (before round 5), slot 1's claim
+    then took a real block and slot 0's came back empty; every wave of the
+    XCD drew a slot-0 ticket and exited, and slot 1's block stayed
+    unwritten (with the delay in every frame; without it in 13 of 1,800
+    first frames of the pad-fill loop above,
+    profiles/r05/wave_queue_claim_order.log).  The framebuffer is filled
+    with a sentinel before every frame, so an unwritten block shows."""
+    import ctypes
+    n, w, h, spp, depth = case
+    sp, al = rt.generate_spheres(n, rt.SEED)
+    hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
+    monkeypatch.setenv("RT_TEST_CLAIM_DELAY", str(delay))  # read at rt_create
+    want = None
+    bad = []
+    for i in range(12):
+        with rt.KernelRenderer(w, h, mode="scene", spp=spp, radiance=True, variant=(0, 13)[i % 2],
+                               pad_fill=i % 3) as r:
+            r.resize(w, h)
+            r.setPosition(rt.camera.scene_pose())
+            r.set_scene(sp, al, max_depth=depth)
+            if want is None:
+                _, K = r.camera()
+                want = oracle.Scene(sp, al, max_depth=depth).render(w, h, rt.camera.scene_pose(), K,
+                                                                     spp=spp)[0]
+            fb = r.framebuffer_ptr()
+            for f in range(3):
+                assert hip.hipMemset(ctypes.c_void_p(fb), 0xAB, ctypes.c_size_t(w * h * 4)) == 0
+                assert hip.hipDeviceSynchronize() == 0
+                r.render(stats=f == 2)
+                img = r.readback()
+                diff = np.any(img != want, axis=-1)
+                if diff.any():
+                    ys, xs = np.nonzero(diff)
+                    bad.append({"renderer": i, "frame": f, "pixels": int(diff.sum()),
+                                "box": [int(xs.min()), int(xs.max()), int(ys.min()), int(ys.max())],
+                                "sentinel": int(np.all(img[diff] == 0xAB))})
+    assert not bad, bad[:5]
+
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,w,h,spp,jitter,tiles", [
