@@ -55,6 +55,8 @@ def load() -> ctypes.CDLL:
                                           ctypes.c_int]),
         "orc_max_threads": (ctypes.c_int, []),
         "orc_cam_screen_check": (None, [_P, _P, _P, _P, _u32, ctypes.c_double, ctypes.c_double, _P]),
+        "orc_shd_screen_check": (None, [_P, _P, _P, _P, _u32, ctypes.c_double, ctypes.c_double,
+                                        ctypes.c_double, _P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -209,4 +211,19 @@ def cam_screen_check(o, dirs, spheres, idx, slack_oc: float, slack_r: float):
     out = np.zeros(3, np.uint64)
     load().orc_cam_screen_check(_p(oa), _p(d), _p(sp), _p(ix), d.shape[0], float(slack_oc),
                                 float(slack_r), _p(out))
+    return int(out[0]), int(out[1]), int(out[2])
+
+
+def shd_screen_check(origins, L, spheres, idx, big_m: float, slack_m: float, grow: float):
+    """Test-only check of the product's light-plane shadow screen (oracle.c
+    orc_shd_screen_check): (exact-accepted pairs the screen rejects, pairs
+    the screen passes, pairs the exact discriminant accepts)."""
+    o = np.ascontiguousarray(origins, np.float32).reshape(-1, 3)
+    la = _f32(L, 3)
+    sp = np.ascontiguousarray(spheres, np.float32).reshape(-1, 4)
+    ix = np.ascontiguousarray(idx, np.uint32).reshape(-1)
+    assert ix.shape[0] == o.shape[0]
+    out = np.zeros(3, np.uint64)
+    load().orc_shd_screen_check(_p(o), _p(la), _p(sp), _p(ix), o.shape[0], float(big_m),
+                                float(slack_m), float(grow), _p(out))
     return int(out[0]), int(out[1]), int(out[2])

@@ -509,6 +509,68 @@ void orc_cam_screen_check(const float o[3], const float* dirs, const float* sp, 
     }
 }
 
+/* Test-only: the product's light-plane shadow screen (rt_kernels.hip walk<>,
+ * shd_screen_kernel; rt_capi.cpp do_render makes the basis) against the
+ * exact discriminant of isect, for m (origin, sphere) pairs with the
+ * frame's shadow direction L.  The basis {e1, e2} is made from L as the host
+ * makes it (f64, rounded to f32); slack_m scales the 2D slack delta =
+ * slack_m u (M + 1e-4) and grow (0 or 4) the radius factors of the record.
+ * out[0] = pairs the exact test accepts and the screen rejects (must be 0),
+ * out[1] = pairs the screen passes, out[2] = pairs the exact test accepts. */
+void orc_shd_screen_check(const float* origins, const float L[3], const float* sp,
+                          const uint32_t* idx, uint32_t m, double big_m, double slack_m,
+                          double grow, uint64_t out[3]) {
+    const double u = 1.0 / 16777216.0;
+    double l[3] = {L[0], L[1], L[2]};
+    const double ln = sqrt(l[0] * l[0] + l[1] * l[1] + l[2] * l[2]);
+    for (int i = 0; i < 3; ++i) l[i] /= ln;
+    int kmin = 0;
+    for (int i = 1; i < 3; ++i)
+        if (fabs(l[i]) < fabs(l[kmin])) kmin = i;
+    double e1[3] = {0.0, 0.0, 0.0};
+    e1[kmin] = 1.0;
+    const double al = l[kmin];
+    for (int i = 0; i < 3; ++i) e1[i] -= al * l[i];
+    const double n1 = sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+    for (int i = 0; i < 3; ++i) e1[i] /= n1;
+    const double e2[3] = {l[1] * e1[2] - l[2] * e1[1], l[2] * e1[0] - l[0] * e1[2],
+                          l[0] * e1[1] - l[1] * e1[0]};
+    float e[6];
+    for (int i = 0; i < 3; ++i) {
+        e[i] = (float)e1[i];
+        e[3 + i] = (float)e2[i];
+    }
+    const double delta = slack_m * u * (big_m + 1e-4);
+    out[0] = out[1] = out[2] = 0;
+    for (uint32_t k = 0; k < m; ++k) {
+        const float* o = origins + 3u * k;
+        const float* s = sp + 4u * idx[k];
+        /* isect's discriminant (rt_kernels.hip isect_h), direction L */
+        const float ocx = o[0] - s[0], ocy = o[1] - s[1], ocz = o[2] - s[2];
+        const float b = fmaf(ocz, L[2], fmaf(ocy, L[1], ocx * L[0]));
+        const float qx = fmaf(-b, L[0], ocx);
+        const float qy = fmaf(-b, L[1], ocy);
+        const float qz = fmaf(-b, L[2], ocz);
+        const float qq = fmaf(qz, qz, fmaf(qy, qy, qx * qx));
+        const float h = fmaf(s[3], s[3], -qq);
+        /* the record (f64, rounded) and the lane's screen (f32, as the kernel) */
+        const double cu = (double)s[0] * e[0] + (double)s[1] * e[1] + (double)s[2] * e[2];
+        const double cv = (double)s[0] * e[3] + (double)s[1] * e[4] + (double)s[2] * e[5];
+        const double rg = (double)s[3] * (1.0 + grow * u) + delta;
+        const double rr = rg * rg * (1.0 + grow * u);
+        float rrf = (float)rr;
+        if ((double)rrf < rr) rrf = nextafterf(rrf, INFINITY); /* toward +inf */
+        const float up = fmaf(o[2], e[2], fmaf(o[1], e[1], o[0] * e[0]));
+        const float vp = fmaf(o[2], e[5], fmaf(o[1], e[4], o[0] * e[3]));
+        const float du = up - (float)cu, dv = vp - (float)cv;
+        const int pass = !(fmaf(dv, dv, du * du) > rrf);
+        const int exact = !(h < 0.0f);
+        out[0] += (uint64_t)(exact && !pass);
+        out[1] += (uint64_t)pass;
+        out[2] += (uint64_t)exact;
+    }
+}
+
 /* ---- octree walk (DESIGN.md "Octree walk") --------------------------------- */
 
 typedef struct {

@@ -34,6 +34,8 @@ hipError_t launch_unpack(const uint32_t* packed, const uint32_t* tiles, uint32_t
                          hipStream_t st);
 hipError_t launch_cam_screen(const float4* prim_sp, uint32_t n, const float o[3], float4* out,
                              hipStream_t st);
+hipError_t launch_shd_screen(const float4* prim_sp, uint32_t n, const float e[6], double delta,
+                             float4* out, hipStream_t st);
 }  // namespace rtamd
 
 using namespace rtamd;
@@ -154,6 +156,11 @@ struct rt_renderer {
     // made for: the scene build and the camera origin
     DevBuf<float4> d_prim_cam;
     uint64_t scene_gen = 0, cam_gen = ~0ull;
+    // light-plane screen records (SceneArgs::prim_shd) and the basis and
+    // scene they were made for
+    DevBuf<float4> d_prim_shd;
+    uint64_t shd_gen = ~0ull;
+    float shd_e[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float cam_o[3] = {0.f, 0.f, 0.f};
     rt_scene_info info{};
     std::string err;
@@ -435,6 +442,14 @@ int build_scene(rt_renderer* r) {
     sc.albedo = r->d_albedo.p;
     sc.max_depth = depth;
     sc.stack_depth = std::max(1u, std::min(depth, in.depth_reached));
+    {
+        // LDS leaf staging while the leaf references fit the L2s (DESIGN.md
+        // 5.1); RT_LDS_STAGE=0 / 1 forces it off / on (A/B and tests)
+        const char* ls = getenv("RT_LDS_STAGE");
+        const bool fits = uint64_t(in.n_prim_refs) * sizeof(float4) <= kLdsStageMaxRefBytes;
+        const bool on = ls && *ls ? atoi(ls) != 0 : fits;
+        sc.lds_max = on ? kLeafBuf : 0u;
+    }
     sc.G = static_cast<float>(1u << depth);
     for (int i = 0; i < 3; ++i) {
         sc.rmin[i] = rmin[i];
@@ -571,6 +586,51 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
             r->cam_gen = r->scene_gen;
         }
         a.sc.prim_cam = r->d_prim_cam.p;
+        // the light-plane screen: an orthonormal basis {e1, e2} of the plane
+        // perpendicular to the shadow direction a.L (in f64 from the f32 L the
+        // kernel uses, then rounded), and the records of its centres, remade
+        // when the scene or the basis changes
+        double l[3] = {a.L[0], a.L[1], a.L[2]};
+        const double ln = sqrt(l[0] * l[0] + l[1] * l[1] + l[2] * l[2]);
+        for (double& x : l) x /= ln;
+        int kmin = 0;
+        for (int i = 1; i < 3; ++i)
+            if (fabs(l[i]) < fabs(l[kmin])) kmin = i;
+        double e1[3] = {0.0, 0.0, 0.0};
+        e1[kmin] = 1.0;
+        const double al = l[kmin];
+        for (int i = 0; i < 3; ++i) e1[i] -= al * l[i];
+        const double n1 = sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+        for (double& x : e1) x /= n1;
+        const double e2[3] = {l[1] * e1[2] - l[2] * e1[1], l[2] * e1[0] - l[0] * e1[2],
+                              l[0] * e1[1] - l[1] * e1[0]};
+        for (int i = 0; i < 3; ++i) {
+            a.shd_e[i] = static_cast<float>(e1[i]);
+            a.shd_e[3 + i] = static_cast<float>(e2[i]);
+        }
+        const float4* before_s = r->d_prim_shd.p;
+        if ((ost = ensure(r, r->d_prim_shd, nr))) return ost;
+        if (r->d_prim_shd.p != before_s || r->shd_gen != r->scene_gen ||
+            memcmp(r->shd_e, a.shd_e, sizeof(r->shd_e)) != 0) {
+            // M bounds |origin| and |centre| of every shadow test: the root
+            // box holds every sphere, and a shadow origin is a hit point
+            // moved 1e-5 off its sphere
+            double m = 0.0;
+            for (int c = 0; c < 8; ++c) {
+                double q = 0.0;
+                for (int i = 0; i < 3; ++i) {
+                    const double v = (c >> i) & 1 ? r->info.root_max[i] : r->info.root_min[i];
+                    q += v * v;
+                }
+                m = std::max(m, sqrt(q));
+            }
+            const double delta = kShadowSlackM / 16777216.0 * (m + 1e-4);
+            hipError_t e = launch_shd_screen(a.sc.prim_sp, nr, a.shd_e, delta, r->d_prim_shd.p, st);
+            if (e != hipSuccess) return hip_fail(r, e, "light-plane screen records");
+            memcpy(r->shd_e, a.shd_e, sizeof(r->shd_e));
+            r->shd_gen = r->scene_gen;
+        }
+        a.sc.prim_shd = r->d_prim_shd.p;
     }
     a.counters = r->counters.p;
     RT_HIP(r, hipMemsetAsync(r->counters.p, 0, words * sizeof(unsigned long long), st));
@@ -791,6 +851,7 @@ int rt_destroy(rt_renderer* r) {
     r->d_spheres.release();
     r->d_albedo.release();
     r->d_prim_cam.release();
+    r->d_prim_shd.release();
     r->gpu_build.release();
     r->cell_table.release();
     if (r->ev0) (void)hipEventDestroy(r->ev0);

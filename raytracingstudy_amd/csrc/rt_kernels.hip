@@ -247,7 +247,6 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
 #ifndef RT_LDS_LEAF
 #define RT_LDS_LEAF 1
 #endif
-constexpr uint32_t kLeafBuf = 32;  // spheres per wave; a leaf of >= kLeafBuf uses global loads
 // Leaves of fewer spheres read them directly: staging adds an LDS round trip
 // to the first chunk, which a leaf of one or two chunks does not win back.
 // Measured (profiles/r05/ldsmin_ab.log, 3 alternating rounds, against no
@@ -310,7 +309,24 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
     // Shadow (any-hit) walks start at hit points and keep the full screen.
     const bool cam = kCamMode != 0 && !kAnyHit;
     const bool cam_exact = cam && kCamMode == 2;  // records {o - c, r}: the tests use them as they are
-    const float4* __restrict__ prim_sp = cam ? S.prim_cam : S.prim_sp;
+    // Light-plane screen: a shadow walk's direction is the
+    // frame's L in every lane, so a sphere is near the ray iff its centre is
+    // near the ray's origin in the plane perpendicular to L.  The records
+    // hold each centre's {u, v} there and a radius grown by the rounding
+    // bound, the lane its origin's {up, vp}: 5 VALU a sphere instead of 13.
+#ifdef RT_NO_SHADOW_SCREEN
+    constexpr bool kShdOk = false;
+#else
+    constexpr bool kShdOk = true;
+#endif
+    const bool shd = kShdOk && kAnyHitT && !kDynAny;
+    float up = 0.0f, vp = 0.0f;
+    if (shd) {
+        KernArgs* ke = kernargs();
+        up = fmaf(o2, ke->shd_e[2], fmaf(o1, ke->shd_e[1], o0 * ke->shd_e[0]));
+        vp = fmaf(o2, ke->shd_e[5], fmaf(o1, ke->shd_e[4], o0 * ke->shd_e[3]));
+    }
+    const float4* __restrict__ prim_sp = cam ? S.prim_cam : shd ? S.prim_shd : S.prim_sp;
     const uint2* __restrict__ nodes = S.nodes;
     const float o[3] = {o0, o1, o2};
     const float d[3] = {d0, d1, d2};
@@ -330,6 +346,11 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         if (a < 1e-20f) a = 1e-20f;
         const float og = neg ? S.G - g : g;
         inv[i] = 1.0f / (a * S.scale[i]);
+        // a shadow walk's direction is the frame's light direction, the same
+        // in every lane (sample_color_unified): its reciprocals live in SGPRs
+        if (kAnyHitT && !kDynAny)
+            inv[i] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
+                                                   __builtin_bit_cast(uint32_t, inv[i])));
         nog[i] = -(og * inv[i]);
         mt |= neg ? ftop << (i * kf) : 0u;
     }
@@ -438,6 +459,11 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                     // rounding bound, so every sphere isect accepts passes
                     const float b = fmaf(sv[q].z, d2, fmaf(sv[q].y, d1, sv[q].x * d0));
                     pos = !(fmaf(b, b, -sv[q].w) < 0.0f);
+                } else if (shd) {
+                    // the centre's light-plane distance from the origin; rr'
+                    // covers the rounding, so every sphere isect accepts passes
+                    const float du = up - sv[q].x, dv = vp - sv[q].y;
+                    pos = !(fmaf(dv, dv, du * du) > sv[q].z);
                 } else {
                     pos = !(isect_h(o0, o1, o2, d0, d1, d2, sv[q]) < 0.0f);
                 }
@@ -450,7 +476,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             if (j + 1u >= cnt) RT_BS(kBsPastEnd);
 #endif
             if (__builtin_expect(__any(maybe), 0)) {
-                if (cam && !cam_exact) {  // the exact tests need the spheres themselves
+                if ((cam && !cam_exact) || shd) {  // the exact tests need the spheres themselves
                     RT_BS(kBsExactLoad);
                     const float4* __restrict__ ex = kernargs()->sc.prim_sp + off;
 #pragma unroll
@@ -481,7 +507,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         // the exact tests skip as before.
         const uint32_t off_u = __builtin_amdgcn_readfirstlane(off);
         const uint32_t cnt_u = __builtin_amdgcn_readfirstlane(cnt);
-        if (cnt_u >= kLdsLeafMin && cnt_u < kLeafBuf && __all(off == off_u)) {
+        if (cnt_u >= kLdsLeafMin && cnt_u < kernargs()->sc.lds_max && __all(off == off_u)) {
             RT_BS(kBsLdsLeaf);
             extern __shared__ __attribute__((aligned(16))) float4 lds_leaf[];
             const uint32_t lb = leaf_buf_base(S, kNoStack);
@@ -768,10 +794,15 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
                 hit = walk<false, kChunk, false, kStats>(S, r0, r1, r2, d0, d1, d2, 0.0f, INFINITY, t,
                                                          idx, n_nodes, n_prims,
                                                          static_cast<uint2*>(stk), false, bs);
-            else
-                hit = walk<true, kChunk, false, kStats>(S, r0, r1, r2, d0, d1, d2, 0.0f, INFINITY, t,
-                                                        idx, n_nodes, n_prims,
+            else {
+                // the shadow direction L is the frame's, the same in every
+                // lane: read afresh from the kernel arguments (SGPRs), not the
+                // lanes' d registers
+                KernArgs* kl = kernargs();
+                hit = walk<true, kChunk, false, kStats>(S, r0, r1, r2, kl->L[0], kl->L[1], kl->L[2],
+                                                        0.0f, INFINITY, t, idx, n_nodes, n_prims,
                                                         static_cast<uint2*>(stk), true, bs);
+            }
         }
         if (phase == 0) {
             hit0 = active && hit;
@@ -1233,42 +1264,51 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
         const uint32_t half = 1u << (ks - 1u);
         // the current slot's grid (packed tile) and origin in wave tiles
         uint32_t cached_s = ~0u, k = 0, sx0 = 0, sy0 = 0, tox = 0, toy = 0, obase = 0;
+        uint32_t owed = 0;  // the last real slot this wave claimed (see below)
         for (;;) {
             uint32_t t = 0;
             if ((threadIdx.x & 63u) == 0) t = static_cast<uint32_t>(atomicAdd(head, 1ull));
             const uint32_t u0 = __builtin_amdgcn_readfirstlane(t) * chunk;
             const uint32_t s = u0 >> ks, w0 = u0 & ((1u << ks) - 1u);
             const bool lead = (threadIdx.x & 63u) == 0;
-            // One claim per slot, in slot order: ticket 0 claims slot 0, and
-            // the ticket holding slot s's middle unit claims slot s + 1 only
-            // AFTER it has seen slot s published.  An XCD's claims are thus
-            // taken from the counter in slot order, so a slot past the last
-            // superblock (kSlotNone) is never followed by a real one.  Claimed
-            // in ticket order instead (before round 5), two claims could
-            // cross at the counter's end: slot s got kSlotNone and slot s + 1
-            // the last block, and when every wave of the XCD had drawn one of
-            // slot s's tickets and exited, no wave was left for that block
-            // (an image block left unwritten; test_gpu_variants.py
-            // test_wave_queue_claims_in_slot_order).  The claim's atomic is
-            // issued after the load that saw slot s published returned, and
-            // that value was stored after slot s's own claim returned: both
-            // returning atomics are performed at the one counter, in that order.
-            if (lead && u0 == 0u) {
+            // The ticket holding slot s's middle unit claims slot s + 1 as soon
+            // as it has its ticket (ticket 0 claims slot 0), before it waits
+            // on anything, so claims run in parallel and land half a slot
+            // early.  Two claims of one XCD can then be taken from the
+            // counter out of slot order: at the counter's end slot s may hold
+            // kSlotNone while slot s + 1 holds the last block.  Round 4's
+            // waves all left at their first empty slot, and that block was
+            // lost when every wave of the XCD had drawn one of slot s's
+            // tickets (13 of 1,800 first frames; test_gpu_variants.py
+            // test_wave_queue_claims_in_slot_order).  Now the wave that
+            // claimed a real slot t (`owed` = t) does not leave before its
+            // tickets reach slot t: every ticket up to there is drawn by a
+            // live wave, so slot t's units all run.  The other waves leave at
+            // their first empty slot as before.  Claiming in slot order (each
+            // claim after the previous slot is published) is correct too but
+            // chains the claims into serial memory round trips, C2 +5..19%;
+            // keeping every wave until two empty slots in a row costs C2
+            // +12% in head atomics (profiles/r05/queue_order_ab.log).
+            uint32_t mine = 0;  // the slot this ticket claimed, if it got a real one
+            if (lead && (u0 == 0u || (w0 <= half && half < w0 + chunk))) {
                 // (test only: hold XCD 0's first claim back until the other
                 // claims of its first slots would have been taken)
-                if (q == 0u)
+                if (q == 0u && u0 == 0u)
                     for (uint32_t d = kernargs()->wq_claim_delay; d; --d) __builtin_amdgcn_s_sleep(127);
+                const uint32_t slot = u0 == 0u ? 0u : s + 1u;
                 const uint32_t g = static_cast<uint32_t>(atomicAdd(claims, 1ull));
-                __hip_atomic_store(slots, g < n1 ? g + 1u : kSlotNone, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+                if (slot < a.wq_slot_stride)
+                    __hip_atomic_store(slots + slot, g < n1 ? g + 1u : kSlotNone, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                if (g < n1) mine = slot;
             }
+            owed = max(owed, __builtin_amdgcn_readfirstlane(mine));
             uint32_t e = kSlotNone;
             if (s != cached_s) {  // resolve the slot's superblock or block (published, or soon)
                 if (lead && s < a.wq_slot_stride) {
-                    // its claimer holds a ticket of slot s - 1 (or ticket 0),
-                    // which waits on nothing later than slot s - 1; the cap
-                    // (~1 s) only turns a broken invariant into a flagged,
-                    // visibly wrong frame, not a hang
+                    // the claimer holds a ticket already and publishes before it
+                    // waits on anything; the cap (~1 s) only turns a broken
+                    // invariant into a flagged, visibly wrong frame, not a hang
                     for (uint32_t spin = 0;; ++spin) {
                         e = __hip_atomic_load(slots + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         if (e != 0u) break;
@@ -1281,12 +1321,7 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
                     }
                 }
                 e = __builtin_amdgcn_readfirstlane(e);
-            }
-            if (lead && u0 != 0u && w0 <= half && half < w0 + chunk) {
-                const uint32_t g = static_cast<uint32_t>(atomicAdd(claims, 1ull));
-                if (s + 1u < a.wq_slot_stride)
-                    __hip_atomic_store(slots + s + 1u, g < n1 ? g + 1u : kSlotNone, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
+                if (e == kSlotNone && s < owed) continue;  // a slot this wave claimed is ahead
             }
             if (s != cached_s) {
 #ifdef RT_TIMELINE
@@ -1462,6 +1497,34 @@ __global__ void __launch_bounds__(kBlockThreads)
     const double u = 1.0 / 16777216.0;  // 2^-24, the f32 unit roundoff
     const double cd = oo - rr - (kScreenSlackOc * u) * oo - (kScreenSlackR * u) * rr;
     out[i] = make_float4(x, y, z, kCamMode == 2 ? c.w : __double2float_rd(cd));
+}
+
+// Light-plane screen records (SceneArgs::prim_shd): per
+// reference the centre's {u, v} = {c.e1, c.e2} (f64, rounded to nearest) and
+// rr' = ((r (1 + 4u) + delta)^2 (1 + 4u)) rounded up, delta = the slack for
+// this scene (kShadowSlackM u M).  One thread per reference.
+__global__ void __launch_bounds__(kBlockThreads)
+    shd_screen_kernel(const float4* __restrict__ prim_sp, uint32_t n, float e0, float e1, float e2,
+                      float e3, float e4, float e5, double delta, float4* __restrict__ out) {
+    const uint32_t i = blockIdx.x * kBlockThreads + threadIdx.x;
+    if (i >= n) return;
+    const float4 c = prim_sp[i];
+    const double u = static_cast<double>(c.x) * e0 + static_cast<double>(c.y) * e1 + static_cast<double>(c.z) * e2;
+    const double v = static_cast<double>(c.x) * e3 + static_cast<double>(c.y) * e4 + static_cast<double>(c.z) * e5;
+    const double ur = 1.0 / 16777216.0;
+    const double rg = static_cast<double>(c.w) * (1.0 + 4.0 * ur) + delta;
+    out[i] = make_float4(static_cast<float>(u), static_cast<float>(v),
+                         __double2float_ru(rg * rg * (1.0 + 4.0 * ur)), 0.0f);
+}
+
+hipError_t launch_shd_screen(const float4* prim_sp, uint32_t n, const float e[6], double delta,
+                             float4* out, hipStream_t st) {
+    if (n) {
+        hipLaunchKernelGGL(shd_screen_kernel, dim3((n + kBlockThreads - 1) / kBlockThreads),
+                           dim3(kBlockThreads), 0, st, prim_sp, n, e[0], e[1], e[2], e[3], e[4], e[5],
+                           delta, out);
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_cam_screen(const float4* prim_sp, uint32_t n, const float o[3], float4* out,

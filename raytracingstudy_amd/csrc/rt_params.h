@@ -191,7 +191,24 @@ struct SceneArgs {
     // (cam_screen_kernel, refreshed when the origin or the scene changes).
     // Primary rays screen a sphere by fma(b, b, -C') >= 0 with b = (o - c).d.
     const float4* prim_cam;
+    // Light-plane screen records (DESIGN.md 5.1 "Light-plane screen"): per leaf
+    // reference {u, v} = the centre's coordinates in the plane perpendicular
+    // to the light direction L (basis FrameArgs::shd_e) and rr' >= (r + slack)^2,
+    // made once per scene and light (shd_screen_kernel).  Shadow rays (any-hit,
+    // direction L) screen a sphere by (u_p - u)^2 + (v_p - v)^2 <= rr'.
+    const float4* prim_shd;
+    // LDS leaf staging: leaves of kLdsLeafMin .. lds_max - 1
+    // spheres are staged; kLeafBuf when the scene's leaf references fit the
+    // L2s, 0 (off) when they outgrow them (build_scene, RT_LDS_STAGE)
+    uint32_t lds_max;
 };
+
+// Spheres per wave in the LDS leaf buffer (a leaf of >= kLeafBuf uses global loads)
+constexpr uint32_t kLeafBuf = 32;
+// Leaf reference bytes (16 each) above which staging is off: the 8 XCDs'
+// 4 MiB L2s together.  C5's 24 MB gains from staging (-7.8%), C5d's 78 MB
+// loses (+2.5%: a staged leaf waits for all of its lines' L2 misses at once)
+constexpr uint64_t kLdsStageMaxRefBytes = 32ull << 20;
 
 // Slack of the camera-relative screen, in units of 2^-24: the
 // screen may only pass MORE spheres than the exact test, so C' undercuts
@@ -199,6 +216,11 @@ struct SceneArgs {
 // (13 u |o - c|^2 + 5 u r^2 derived there; 16 and 8 kept).
 constexpr double kScreenSlackOc = 16.0;
 constexpr double kScreenSlackR = 8.0;
+// Slack of the light-plane screen: an accepted sphere's
+// centre lies within r (1 + 3.5 u) + 7.8 u M of the shadow ray's origin in
+// the light plane (M bounds |origin| and |centre|: the root box's farthest
+// corner); the records use r (1 + 4 u) + 64 u M.
+constexpr double kShadowSlackM = 64.0;
 
 struct FrameArgs {
     CamArgs cam;
@@ -210,6 +232,7 @@ struct FrameArgs {
     uint32_t shadows;
     uint32_t contract;  // compat: 1 = getRay with nvcc-style FMA contraction (RT_FLAG_COMPAT_FMA)
     float L[3];         // unit vector toward the light
+    float shd_e[6];     // light-plane basis {e1, e2} (orthonormal, perpendicular to L; f32)
     float ambient;
     float inv_spp;      // 1 / samples in the image (all accumulated frames)
     // progressive accumulation (RT_FLAG_PROGRESSIVE)

@@ -107,3 +107,92 @@ def test_slack_costs_a_thin_annulus(which, bound):
     d, idx = _silhouette_rays(CAMERAS[0], sp, 400_000, rng, 0.5)
     miss, passed, exact = oracle.cam_screen_check(CAMERAS[0], d, sp, idx, SLACK_OC, SLACK_R)
     assert miss == 0 and exact <= passed <= bound * exact, (passed / exact)
+
+
+# ---- light-plane shadow screen (DESIGN.md 5.1 "Light-plane screen") --------
+
+SLACK_M, GROW = 64.0, 4.0  # rt_params.h kShadowSlackM; shd_screen_kernel's r (1 + 4u) and (1 + 4u)
+
+
+def _kernel_light(ld):
+    """FrameArgs::L as rt_capi.cpp fill_frame_args makes it: -(ld / |ld|) in f32."""
+    ld = np.asarray(ld, np.float32)
+    ll = np.sqrt((ld[0] * ld[0] + ld[1] * ld[1]) + ld[2] * ld[2])
+    return (-(ld / ll)).astype(np.float32)
+
+
+def _shadow_pairs(sp, L, n, rng, spread, big_m):
+    """n shadow-ray origins whose rays (direction L) pass sphere idx[k] at
+    r (1 + xi) from its centre, xi ~ U[-spread, spread], the origin anywhere
+    along the line within the scene's bound M (in front of or behind it)."""
+    l = L.astype(np.float64) / np.linalg.norm(L.astype(np.float64))
+    a = np.array([1.0, 0.0, 0.0]) if abs(l[0]) < 0.9 else np.array([0.0, 1.0, 0.0])
+    e1 = a - (a @ l) * l
+    e1 /= np.linalg.norm(e1)
+    e2 = np.cross(l, e1)
+    idx = rng.integers(0, sp.shape[0], n)
+    c = sp[idx, :3].astype(np.float64)
+    r = sp[idx, 3].astype(np.float64)
+    th = rng.uniform(0, 2 * np.pi, n)
+    xi = rng.uniform(-spread, spread, n)
+    w = (np.cos(th)[:, None] * e1 + np.sin(th)[:, None] * e2) * (r * (1.0 + xi))[:, None]
+    s = rng.uniform(-1.0, 1.0, n)
+    o = (c + w + s[:, None] * l).astype(np.float32)
+    keep = np.linalg.norm(o.astype(np.float64), axis=1) <= big_m
+    return o[keep], idx[keep]
+
+
+def _bound(sp):
+    lo = (sp[:, :3] - sp[:, 3:]).min(0).astype(np.float64)
+    hi = (sp[:, :3] + sp[:, 3:]).max(0).astype(np.float64)
+    return max(np.linalg.norm(np.where([(c >> i) & 1 for i in range(3)], hi, lo)) for c in range(8))
+
+
+LIGHTS = [(1.0, 1.0, -1.0),      # the default (SURVEY 8d)
+          (0.3, -2.0, 0.7), (0.0, 0.0, 1.0), (-1.0, 1e-3, 0.2)]
+
+
+@pytest.mark.parametrize("ld", LIGHTS)
+def test_shadow_screen_never_rejects_an_accepted_sphere(spheres, ld):
+    """The light-plane screen at the product's slack passes every sphere whose
+    exact discriminant (isect, direction L) accepts it, for shadow rays passing
+    sphere silhouettes; at zero slack it misses some (the check has teeth)."""
+    L = _kernel_light(ld)
+    big_m = _bound(spheres)
+    rng = np.random.default_rng(11)
+    miss = passed = exact = miss0 = 0
+    for spread in (1e-7, 1e-6, 1e-5, 1e-3, 0.3):
+        o, idx = _shadow_pairs(spheres, L, 200_000, rng, spread, big_m)
+        m, p, e = oracle.shd_screen_check(o, L, spheres, idx, big_m, SLACK_M, GROW)
+        miss += m
+        passed += p
+        exact += e
+        miss0 += oracle.shd_screen_check(o, L, spheres, idx, big_m, 0.0, 0.0)[0]
+    assert miss == 0, f"shadow screen rejected {miss} exactly-accepted pairs"
+    assert exact > 0 and passed >= exact
+    if np.count_nonzero(ld) > 1:  # an axis-aligned L makes both forms exact
+        assert miss0 > 0, "zero slack should miss some silhouette pairs"
+
+
+def test_shadow_screen_annulus():
+    """What the slack costs: shadow rays spread uniformly over discs of 1.5
+    radii around C3's and C5's spheres pass the screen at most a few percent
+    more often than the exact test accepts them."""
+    L = _kernel_light((1.0, 1.0, -1.0))
+    rng = np.random.default_rng(3)
+    for n_sph in (100_000, 1_000_000):
+        sp, _ = rt.generate_spheres(n_sph, rt.SEED)
+        big_m = _bound(sp)
+        o, idx = _shadow_pairs(sp, L, 400_000, rng, 0.0, big_m)
+        # redraw each pair's offset uniformly over the disc of radius 1.5 r
+        l = L.astype(np.float64) / np.linalg.norm(L.astype(np.float64))
+        c = sp[idx, :3].astype(np.float64)
+        t = (o.astype(np.float64) - c) @ l
+        w = o.astype(np.float64) - c - t[:, None] * l
+        w /= np.linalg.norm(w, axis=1)[:, None]
+        rad = sp[idx, 3].astype(np.float64) * np.sqrt(rng.uniform(0, 2.25, len(idx)))
+        o2 = (c + w * rad[:, None] + t[:, None] * l).astype(np.float32)
+        m, p, e = oracle.shd_screen_check(o2, L, sp, idx, big_m, SLACK_M, GROW)
+        assert m == 0
+        print(n_sph, "passed / accepted", p / e)
+        assert p <= 1.05 * e, (n_sph, p, e)

@@ -120,6 +120,37 @@ def test_wave_queue_claims_in_slot_order(gpu, oracle, case, delay, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("case", [(20000, 64, 48, 64, 7), (20000, 128, 96, 2, 12),
+                                  (30000, 40, 30, 256, 12)],
+                         ids=lambda c: "n%d_%dx%d_s%d_d%d" % c)
+def test_lds_staging_on_and_off(gpu, oracle, case, monkeypatch):
+    """LDS leaf staging (scene-level switch, rt_params.h kLdsStageMaxRefBytes)
+    changes which path reads a leaf's spheres, never what a frame computes:
+    forced on and forced off (RT_LDS_STAGE, read when the scene is built),
+    plain and stats frames give the oracle's image and counters."""
+    n, w, h, spp, depth = case
+    sp, al = rt.generate_spheres(n, rt.SEED)
+    out = {}
+    for stage in ("0", "1"):
+        monkeypatch.setenv("RT_LDS_STAGE", stage)
+        with rt.KernelRenderer(w, h, mode="scene", spp=spp, radiance=True) as r:
+            r.resize(w, h)
+            r.setPosition(rt.camera.scene_pose())
+            r.set_scene(sp, al, max_depth=depth)
+            r.render()
+            img0 = r.readback()
+            st = r.render(stats=True)
+            img, rad = r.readback(), r.readback_radiance()
+            _, K = r.camera()
+        out[stage] = (img0, img, rad, st)
+    ref = oracle.Scene(sp, al, max_depth=depth).render(w, h, rt.camera.scene_pose(), K, spp=spp)
+    for stage, (img0, img, rad, st) in out.items():
+        rep = vc.diff_report(img, rad, st, ref)
+        assert not rep, (stage, rep)
+        assert np.array_equal(img0, img), stage
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,w,h,spp,jitter,tiles", [
     (30000, 70, 45, 256, None, False),   # four rounds (C5's shape), edge pixels
     (30000, 70, 45, 192, None, True),    # three rounds, packed tiles with off-image pixels
