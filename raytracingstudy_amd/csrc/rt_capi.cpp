@@ -443,12 +443,10 @@ int build_scene(rt_renderer* r) {
     sc.max_depth = depth;
     sc.stack_depth = std::max(1u, std::min(depth, in.depth_reached));
     {
-        // LDS leaf staging while the leaf references fit the L2s (DESIGN.md
-        // 5.1); RT_LDS_STAGE=0 / 1 forces it off / on (A/B and tests)
+        // LDS leaf staging on every scene; RT_LDS_STAGE=0
+        // turns it off (A/B and the on/off parity test)
         const char* ls = getenv("RT_LDS_STAGE");
-        const bool fits = uint64_t(in.n_prim_refs) * sizeof(float4) <= kLdsStageMaxRefBytes;
-        const bool on = ls && *ls ? atoi(ls) != 0 : fits;
-        sc.lds_max = on ? kLeafBuf : 0u;
+        sc.lds_max = ls && *ls && atoi(ls) == 0 ? 0u : kLeafBuf;
     }
     sc.G = static_cast<float>(1u << depth);
     for (int i = 0; i < 3; ++i) {

@@ -319,7 +319,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
 #else
     constexpr bool kShdOk = true;
 #endif
-    const bool shd = kShdOk && kAnyHitT && !kDynAny;
+    const bool shd = kShdOk && kAnyHit;  // every any-hit walk is a shadow ray along L
     float up = 0.0f, vp = 0.0f;
     if (shd) {
         KernArgs* ke = kernargs();

@@ -198,17 +198,14 @@ struct SceneArgs {
     // direction L) screen a sphere by (u_p - u)^2 + (v_p - v)^2 <= rr'.
     const float4* prim_shd;
     // LDS leaf staging: leaves of kLdsLeafMin .. lds_max - 1
-    // spheres are staged; kLeafBuf when the scene's leaf references fit the
-    // L2s, 0 (off) when they outgrow them (build_scene, RT_LDS_STAGE)
+    // spheres are staged; kLeafBuf, or 0 (off) under RT_LDS_STAGE=0 (A/B:
+    // off at run time loses on every config, C5d included,
+    // profiles/r05/stage_switch_ab.log)
     uint32_t lds_max;
 };
 
 // Spheres per wave in the LDS leaf buffer (a leaf of >= kLeafBuf uses global loads)
 constexpr uint32_t kLeafBuf = 32;
-// Leaf reference bytes (16 each) above which staging is off: the 8 XCDs'
-// 4 MiB L2s together.  C5's 24 MB gains from staging (-7.8%), C5d's 78 MB
-// loses (+2.5%: a staged leaf waits for all of its lines' L2 misses at once)
-constexpr uint64_t kLdsStageMaxRefBytes = 32ull << 20;
 
 // Slack of the camera-relative screen, in units of 2^-24: the
 // screen may only pass MORE spheres than the exact test, so C' undercuts

@@ -124,10 +124,10 @@ def test_wave_queue_claims_in_slot_order(gpu, oracle, case, delay, monkeypatch):
                                   (30000, 40, 30, 256, 12)],
                          ids=lambda c: "n%d_%dx%d_s%d_d%d" % c)
 def test_lds_staging_on_and_off(gpu, oracle, case, monkeypatch):
-    """LDS leaf staging (scene-level switch, rt_params.h kLdsStageMaxRefBytes)
-    changes which path reads a leaf's spheres, never what a frame computes:
-    forced on and forced off (RT_LDS_STAGE, read when the scene is built),
-    plain and stats frames give the oracle's image and counters."""
+    """LDS leaf staging changes which path reads a leaf's spheres, never what
+    a frame computes: on (the default) and off (RT_LDS_STAGE=0, read when
+    the scene is built), plain and stats frames give the oracle's image and
+    counters."""
     n, w, h, spp, depth = case
     sp, al = rt.generate_spheres(n, rt.SEED)
     out = {}
