@@ -507,7 +507,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         // the exact tests skip as before.
         const uint32_t off_u = __builtin_amdgcn_readfirstlane(off);
         const uint32_t cnt_u = __builtin_amdgcn_readfirstlane(cnt);
-        if (cnt_u >= kLdsLeafMin && cnt_u < kLeafBuf && __all(off == off_u)) {
+        if (cnt_u >= kLdsLeafMin && cnt_u < kernargs()->sc.lds_max && __all(off == off_u)) {
             RT_BS(kBsLdsLeaf);
             extern __shared__ __attribute__((aligned(16))) float4 lds_leaf[];
             const uint32_t lb = leaf_buf_base(S, kNoStack);
