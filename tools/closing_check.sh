@@ -2,11 +2,11 @@
 # Closing check at the current tree (run from the repo root via gpurun): the GPU
 # test suite, smoke(), the default bench line, and a rocprofv3 kernel trace of
 # the headline bench (C3 only) whose average scene-kernel duration must agree
-# with the bench line's HIP-event kernel_ms.  Outputs under gpurun_out/r04z/.
+# with the bench line's HIP-event kernel_ms.  Outputs under $OUT (default gpurun_out/closing/).
 # usage: bash tools/closing_check.sh
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r04z
+OUT=${OUT:-gpurun_out/closing}
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
 tail -n 2 $OUT/pytest.log
