@@ -205,10 +205,7 @@ struct SceneArgs {
 };
 
 // Spheres per wave in the LDS leaf buffer (a leaf of >= kLeafBuf uses global loads)
-#ifndef RT_LEAF_BUF
-#define RT_LEAF_BUF 32
-#endif
-constexpr uint32_t kLeafBuf = RT_LEAF_BUF;
+constexpr uint32_t kLeafBuf = 32;
 
 // Slack of the camera-relative screen, in units of 2^-24: the
 // screen may only pass MORE spheres than the exact test, so C' undercuts
