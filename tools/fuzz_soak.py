@@ -3,7 +3,10 @@ the suite runs (seeds FROM..TO), each rendered as a plain frame into a
 sentinel-filled framebuffer and then as a stats frame, against the oracle
 (RGBA8, radiance, the four counters).  Prints each mismatch and a summary.
 
-    python tools/fuzz_soak.py [FROM=64] [TO=1064]
+    python tools/fuzz_soak.py [FROM=64] [TO=1064] [BUDGET_S=400]
+
+Prints one line per seed (the box kills a silent run), and stops once the
+time budget is spent.
 """
 import ctypes
 import json
@@ -22,10 +25,15 @@ from test_gpu_parity import _fuzz_case  # noqa: E402
 
 lo = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 hi = int(sys.argv[2]) if len(sys.argv) > 2 else 1064
+budget = float(sys.argv[3]) if len(sys.argv) > 3 else 400.0
 oracle.load()
 hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
 bad, t0 = [], time.time()
+done = 0
 for seed in range(lo, hi):
+    if time.time() - t0 > budget:
+        break
+    t1 = time.time()
     c = _fuzz_case(seed)
     with rt.KernelRenderer(c["w"], c["h"], mode="scene", spp=c["spp"], radiance=True,
                            shadows=c["shadows"], jitter=c["jitter"], light_dir=c["light"],
@@ -58,9 +66,9 @@ for seed in range(lo, hi):
     if rep:
         bad.append(seed)
         print(json.dumps({"seed": seed, **rep}), flush=True)
-    if (seed - lo) % 10 == 9:
-        print(json.dumps({"done": seed - lo + 1, "bad": len(bad), "s": round(time.time() - t0, 1)}),
-              flush=True)
-print(json.dumps({"lib": os.path.basename(rt._lib.LIB_PATH), "seeds": [lo, hi], "bad": bad,
+    done += 1
+    print(json.dumps({"seed": seed, "ok": not rep, "n": c["n"], "spp": c["spp"], "depth": c["depth"],
+                      "leaf": c["leaf"], "s": round(time.time() - t1, 2)}), flush=True)
+print(json.dumps({"lib": os.path.basename(rt._lib.LIB_PATH), "seeds": [lo, lo + done], "bad": bad,
                   "s": round(time.time() - t0, 1)}))
 sys.exit(1 if bad else 0)
