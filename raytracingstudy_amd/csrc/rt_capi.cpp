@@ -292,6 +292,9 @@ void fill_frame_args(rt_renderer* r, FrameArgs& a) {
     a.variant = v ? v : (a.spp >= 8u ? kVariantWaveQ : kVariantWaveQLow);
 }
 
+// Largest host fallback build attempted (build_scene)
+constexpr uint64_t kHostBuildMaxBytes = 16ull << 30;
+
 // Build the octree of the device sphere list (d_spheres) and point the
 // kernel's scene arguments at it.  The device builder is the default; the
 // host builder (RT_FLAG_HOST_BUILD) yields the identical tree.
@@ -328,12 +331,17 @@ int build_scene(rt_renderer* r) {
             // (rt_scene_info.builder then reports RT_BUILDER_HOST).  Bound the
             // attempt first: the host builder holds at least the overflowing
             // level's references (index + sphere record + per-level lists,
-            // ~64 B each); refuse at once rather than page for minutes
+            // ~64 B each); refuse at once rather than page for minutes.  The
+            // bound is half the host's memory and at most kHostBuildMaxBytes:
+            // a level that overflows 2^32 flag slots has >= 2^29 references,
+            // which the host builder would grind through for minutes (and it
+            // refuses past 2^31 references anyway)
             (void)hipGetLastError();
             const uint64_t need = res.ref_overflow * 64ull;
             const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGE_SIZE);
-            const uint64_t phys = pages > 0 && psz > 0 ? uint64_t(pages) * uint64_t(psz) : 0ull;
-            if (phys && need > phys / 2)
+            uint64_t limit = pages > 0 && psz > 0 ? uint64_t(pages) * uint64_t(psz) / 2 : 0ull;
+            if (!limit || limit > kHostBuildMaxBytes) limit = kHostBuildMaxBytes;
+            if (need > limit)
                 return fail(r, RT_E_NOMEM,
                             "scene too large for the octree: the device builder overflowed at " +
                                 std::to_string(res.ref_overflow) +

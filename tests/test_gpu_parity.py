@@ -744,6 +744,22 @@ def test_scene_fuzz(gpu, oracle, seed):
     _check_counts(st, cnt, 0)
 
 
+def test_tree_past_the_builders_limits_is_refused_quickly(gpu, oracle):
+    """Fuzz seed 66 (3,000 spheres up to 0.25 wide, depth 12, leaf capacity
+    5) needs billions of references: the oracle refuses it (and aborts, so
+    it is not called here), and so must the library, at once.  Before round
+    5 the device builder's overflow fell back to the host builder whenever
+    half the host's memory looked big enough, and on the GPU box (terabytes
+    of RAM) it ground for minutes."""
+    import time
+    c = _fuzz_case(66)
+    with rt.KernelRenderer(c["w"], c["h"], mode="scene", spp=c["spp"]) as r:
+        t0 = time.time()
+        with pytest.raises(rt._lib.RtError, match="scene too large"):
+            r.set_scene(c["sp"], c["al"], max_depth=c["depth"], leaf_capacity=c["leaf"])
+        assert time.time() - t0 < 60
+
+
 def test_device_build_falls_back_to_host_build(gpu, oracle):
     """When the device builder refuses a tree (its per-level reference slots are
     32-bit), rt_set_scene builds the identical tree on the host instead of
