@@ -464,6 +464,10 @@ def run_native(args) -> int:
     # handle waits after each), the frame against one renderer's whole frame,
     # and devices[0]'s own tiles rendered alone for its counters
     per = []
+    try:  # frames record timing events from the first rt_get_multi_timing call on
+        r.multi_timing()
+    except rt._lib.RtError:
+        pass
     for _ in range(5):
         r.render()
         per.append(r.multi_timing())

@@ -94,6 +94,15 @@ enum {
      * (DESIGN.md §4): 0 zero spheres (default), 1 NaN spheres, 2 spheres
      * covering the root box.  Images and counters are the same for all three. */
     RT_FLAG_PAD_FILL_SHIFT = 8,
+    /* Test-only: rt_create / rt_create_multi honour the RT_TEST_* environment
+     * variables (RT_TEST_FAULT fault injection, RT_TEST_CLAIM_DELAY); without
+     * this flag they are ignored (a set one is named on stderr once). */
+    RT_FLAG_TEST_HOOKS = 1u << 10,
+    /* Test-only: before every frame, fill the frame's outputs with a sentinel
+     * (RGBA8 bytes 0xAB, frame or packed tiles; radiance and a first
+     * progressive frame's sums all-ones bits, a NaN), so a pixel the kernels
+     * do not write shows in any readback.  Costs a memset per frame. */
+    RT_FLAG_TEST_POISON = 1u << 11,
     /* bits 16..19: scene-kernel variant for A/B runs (0 = default: 13, the
      * per-wave queue, for spp >= 8, else 7; others in DESIGN.md 5.1); images
      * and counters are identical across variants (packets: images only) */
@@ -225,7 +234,13 @@ int rt_load_spheres(const char* path, float* spheres_out, uint32_t* albedo_out,
 /* Render one frame.  dev_rgba8: W*H*4 device bytes (e.g. the pointer a GL PBO
  * maps to), or NULL to render into the renderer's internal framebuffer.
  * stream: a hipStream_t or NULL (the renderer's own stream).  Asynchronous
- * unless stats != NULL (then it waits for the frame and fills the counters). */
+ * unless stats != NULL (then it waits for the frame and fills the counters).
+ * An earlier frame that the kernel found incomplete (its work queue's bounded
+ * wait gave up: a broken invariant, never a normal frame) is reported by the
+ * first call that sees it, without a sync: this rt_render returns RT_E_HIP
+ * naming that frame and renders nothing, so a caller that never reads back
+ * (the reference's Displayer, src/window/displayer.cpp:51-53) still learns
+ * of it; rt_synchronize, rt_readback and stats frames report it too. */
 int rt_render(rt_renderer* r, void* dev_rgba8, void* stream, rt_stats* stats);
 /* GL interop.  The Displayer registers its PBO with
  * hipGraphicsGLRegisterBuffer (where it called cudaGraphicsGLRegisterBuffer,
@@ -330,10 +345,12 @@ typedef struct rt_multi_info {
  * output stream on devices[0], which is not devices[0]'s render stream, so
  * frame j+1's tiles there do not wait for frame j's unpack.  A failure on one
  * device names it in rt_last_error: "(device <ordinal>, peer <k>)".
- * Test-only: the environment variable RT_TEST_FAULT, read here, injects one
- * failure: "create:k" (peer k's renderer), "comm" (ncclCommInitAll), "slab:k"
- * (peer k's slab allocation) or "queue:k" (peer k's frames flag their
- * wave-queue error, which rt_synchronize / rt_readback report as RT_E_HIP). */
+ * Test-only (with RT_FLAG_TEST_HOOKS): the environment variable RT_TEST_FAULT,
+ * read here, injects one failure: "create:k" (peer k's renderer), "comm"
+ * (ncclCommInitAll), "slab:k" (peer k's slab allocation) or "queue:k" (peer
+ * k's plain frames report themselves incomplete, which the next rt_render,
+ * rt_synchronize or rt_readback returns as RT_E_HIP naming the peer); rt_create
+ * honours "queue:0" for a single-device renderer. */
 int rt_create_multi(const rt_config* cfg, const int32_t* devices, uint32_t n_devices,
                     uint32_t transport, rt_renderer** out);
 int rt_get_multi_info(const rt_renderer* r, rt_multi_info* info);
@@ -341,8 +358,10 @@ int rt_get_multi_info(const rt_renderer* r, rt_multi_info* info);
  * work): render_ms[k] = device k rendering its tiles into its slab (HIP
  * events on its render stream); deliver_ms = on devices[0], from the end of
  * its own tiles to the frame unpacked (the other slabs' arrival over the
- * transport, then the one unpack).  RT_E_STATE for a single-device handle or
- * before the first frame. */
+ * transport, then the one unpack).  Frames record timing events only after
+ * the handle's first rt_get_multi_timing call (the frame path's own
+ * synchronisation events stay timing-free), so that first call, like one for
+ * a single-device handle or an untimed last frame, returns RT_E_STATE. */
 typedef struct rt_multi_timing {
     uint32_t n_devices;
     uint64_t frame;                   /* 0-based index of the frame timed           */

@@ -36,6 +36,8 @@ RT_BUILDER_DEVICE = 0
 RT_BUILDER_HOST = 1
 RT_TILE_SKIP = 0xFFFFFFFF  # rt_unpack_tiles: a padding slot, not copied
 RT_FLAG_PAD_FILL_SHIFT = 8  # test-only: 0 zeros, 1 NaN, 2 covering spheres after the last leaf
+RT_FLAG_TEST_HOOKS = 1 << 10   # test-only: honour the RT_TEST_* environment variables
+RT_FLAG_TEST_POISON = 1 << 11  # test-only: sentinel-fill every frame's outputs first
 RT_FLAG_VARIANT_SHIFT = 16
 RT_FLAG_OPT_SHIFT = 20
 RT_FLAG_CELL_TABLE_SHIFT = 28
@@ -205,6 +207,12 @@ SIGNATURES = {
 
 _lock = threading.Lock()
 _lib = None
+
+# Flags OR-ed into every renderer's rt_config by KernelRenderer.  0 in the
+# product; the test suite sets RT_FLAG_TEST_HOOKS | RT_FLAG_TEST_POISON
+# (tests/conftest.py), so every frame it renders starts from a sentinel-filled
+# framebuffer and the RT_TEST_* hooks are honoured.
+test_flags = 0
 
 # the sources the scene kernel's machine code is built from (device code and
 # its compile flags): a PMC summary is valid for a build iff its stamp matches

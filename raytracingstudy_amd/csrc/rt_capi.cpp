@@ -55,21 +55,29 @@ struct MultiState {
     // for frame j's unpack does not hold frame j+1's tiles on device 0.
     hipStream_t out = nullptr;
     // per frame slot f: each device's packed slab, devices[0]'s receive buffer
-    // of n slabs end to end, and the events that order their reuse (started /
-    // rendered / unpacked also time the frame: rt_get_multi_timing)
+    // of n slabs end to end, and the events that order their reuse (all
+    // timing-disabled: they are waited on every frame)
     std::vector<void*> slab[F];
     void* recv[F] = {nullptr, nullptr};
-    std::vector<hipEvent_t> started[F], rendered[F], sent[F];
+    std::vector<hipEvent_t> rendered[F], sent[F];
     hipEvent_t recvd[F] = {nullptr, nullptr}, unpacked[F] = {nullptr, nullptr}, out_ready = nullptr;
     bool used[F] = {false, false};
+    // rt_get_multi_timing: timing events, recorded only once the caller has
+    // asked for timing: device k's render start / end, devices[0]'s
+    // unpack end; timed[f] = slot f's frame recorded them
+    bool timing = false;
+    bool timed[F] = {false, false};
+    std::vector<hipEvent_t> t_start[F], t_end[F];
+    hipEvent_t t_unpacked[F] = {nullptr, nullptr};
     uint64_t frame = 0;
     // a resize that failed part-way leaves the devices at different sizes:
     // rt_render refuses the handle until a resize succeeds
     bool broken = false;
-    // test-only fault injection (RT_TEST_FAULT, read once by rt_create_multi):
-    // "create:k" peer k's rt_create fails, "comm" ncclCommInitAll fails,
-    // "slab:k" the slab allocation on peer k fails, "queue:k" peer k's frames
-    // flag their wave-queue error word (as a slot that was never published)
+    // test-only fault injection (RT_TEST_FAULT with RT_FLAG_TEST_HOOKS, read
+    // once by rt_create_multi): "create:k" peer k's rt_create fails, "comm"
+    // ncclCommInitAll fails, "slab:k" the slab allocation on peer k fails,
+    // "queue:k" peer k's plain frames report themselves incomplete (as a
+    // slot that was never published: rt_renderer::test_fault_queue)
     enum Fault { kNone = 0, kCreate, kComm, kSlab, kQueue };
     int fault = kNone;
     uint32_t fault_k = 0;
@@ -108,9 +116,16 @@ struct rt_renderer {
     hipEvent_t done = nullptr;
     hipStream_t last_stream = nullptr;
     bool pending = false;
-    // the last frame ran on the wave queue: rt_synchronize / rt_readback check
-    // its 'slot never published' flag (stats frames check it themselves)
-    bool check_queue = false;
+    // wave-queue failure report (FrameArgs::qerr): a pinned host-coherent word
+    // the kernel stores a failed frame's id into; the host reports each new
+    // value once (queue_report), from rt_render without any copy or sync
+    uint32_t* qerr_host = nullptr;
+    uint32_t* qerr_dev = nullptr;
+    uint32_t frame_seq = 0;   // last frame id handed out (never 0)
+    uint32_t qerr_seen = 0;   // last reported value of *qerr_host
+    // test only (RT_TEST_FAULT=queue:k, RT_FLAG_TEST_HOOKS): plain frames
+    // report themselves failed
+    bool test_fault_queue = false;
     float pose[16];
     float K[9];
     uint32_t W = 0, H = 0;
@@ -140,7 +155,8 @@ struct rt_renderer {
     uint32_t n_spheres = 0;
     std::vector<float> spheres;
     bool host_copy = false;
-    // test only: RT_TEST_CLAIM_DELAY at rt_create (FrameArgs::wq_claim_delay)
+    // test only: RT_TEST_CLAIM_DELAY at rt_create with RT_FLAG_TEST_HOOKS
+    // (FrameArgs::wq_claim_delay)
     uint32_t test_claim_delay = 0;
     rt_octree_params oct;
     bool has_scene = false;
@@ -175,6 +191,7 @@ namespace {
 int multi_render(rt_renderer* r, uint32_t* out, hipStream_t hs, rt_stats* stats);
 int multi_wait(rt_renderer* r);
 int multi_synchronize(rt_renderer* r);
+int multi_queue_report(rt_renderer* r);
 void multi_destroy(rt_renderer* r);
 int multi_set_scene_device(rt_renderer* r, uint32_t n, const rt_octree_params* oct);
 // " (device <ordinal>, peer <k>)": names the device in a multi-device error
@@ -278,6 +295,9 @@ void fill_frame_args(rt_renderer* r, FrameArgs& a) {
     a.counters = r->counters.p;
     a.sc.opt = (r->cfg.flags >> RT_FLAG_OPT_SHIFT) & 0xFFu;
     a.wq_claim_delay = r->test_claim_delay;
+    a.qerr = r->qerr_dev;
+    if (++r->frame_seq == 0) r->frame_seq = 1;
+    a.frame_id = r->frame_seq;
     const uint32_t v = (r->cfg.flags >> RT_FLAG_VARIANT_SHIFT) & 0xFu;
     // default: multi-sample frames are scheduled per wave over per-XCD queues
     // (variant 13: C5 -15%, equal on C3, better on multi-GPU shares); 1-spp
@@ -292,8 +312,27 @@ void fill_frame_args(rt_renderer* r, FrameArgs& a) {
     a.variant = v ? v : (a.spp >= 8u ? kVariantWaveQ : kVariantWaveQLow);
 }
 
-// Largest host fallback build attempted (build_scene)
-constexpr uint64_t kHostBuildMaxBytes = 16ull << 30;
+// A test hook's environment variable (RT_TEST_*): its value when the config
+// carries RT_FLAG_TEST_HOOKS, else NULL.  Either way a set variable is named
+// on stderr once per process, so a stray one is visible.
+const char* test_env(uint32_t flags, const char* name) {
+    const char* v = getenv(name);
+    if (!v || !*v) return nullptr;
+    const bool on = (flags & RT_FLAG_TEST_HOOKS) != 0;
+    static std::mutex mu;
+    static std::vector<std::string> said;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        const std::string key = std::string(name) + (on ? "+" : "-");
+        if (std::find(said.begin(), said.end(), key) == said.end()) {
+            said.push_back(key);
+            fprintf(stderr, on ? "librt_amd: test hook %s=%s active (RT_FLAG_TEST_HOOKS)\n"
+                               : "librt_amd: %s=%s ignored (test hooks need RT_FLAG_TEST_HOOKS)\n",
+                    name, v);
+        }
+    }
+    return on ? v : nullptr;
+}
 
 // Build the octree of the device sphere list (d_spheres) and point the
 // kernel's scene arguments at it.  The device builder is the default; the
@@ -324,30 +363,30 @@ int build_scene(rt_renderer* r) {
         hipError_t e = r->gpu_build.build(r->d_spheres.p, n, p.min, p.max, depth, cap, r->stream, &res);
         if (res.n_invalid)
             return fail(r, RT_E_INVALID, "scene has spheres with radius <= 0 or non-finite values");
-        if ((r->cfg.flags >> RT_FLAG_OPT_SHIFT) & kOptDeviceBuildRefuse) res.ref_overflow = 1;
-        if (res.ref_overflow || e == hipErrorOutOfMemory) {
-            // the device builder's 32-bit per-level slots (or HBM) cannot hold
-            // this tree: build the identical tree on the host instead
-            // (rt_scene_info.builder then reports RT_BUILDER_HOST).  Bound the
-            // attempt first: the host builder holds at least the overflowing
-            // level's references (index + sphere record + per-level lists,
-            // ~64 B each); refuse at once rather than page for minutes.  The
-            // bound is half the host's memory and at most kHostBuildMaxBytes:
-            // a level that overflows 2^32 flag slots has >= 2^29 references,
-            // which the host builder would grind through for minutes (and it
-            // refuses past 2^31 references anyway)
+        // (test only: kOptDeviceBuildRefuse makes the device build report
+        // running out of HBM, the one case that falls back to the host)
+        if ((r->cfg.flags >> RT_FLAG_OPT_SHIFT) & kOptDeviceBuildRefuse) e = hipErrorOutOfMemory;
+        if (res.ref_overflow) {
+            // The device builder's 32-bit per-level slots overflowed: that
+            // level holds >= 2^29 references (octree_build.hip), which the
+            // host builder would need >= 2^29 x ~64 B = 32 GiB for (index,
+            // sphere record, per-level lists) and would grind through for
+            // minutes.  Always refused, at once; the
+            // host fallback covers only the device build running out of HBM.
             (void)hipGetLastError();
-            const uint64_t need = res.ref_overflow * 64ull;
-            const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGE_SIZE);
-            uint64_t limit = pages > 0 && psz > 0 ? uint64_t(pages) * uint64_t(psz) / 2 : 0ull;
-            if (!limit || limit > kHostBuildMaxBytes) limit = kHostBuildMaxBytes;
-            if (need > limit)
-                return fail(r, RT_E_NOMEM,
-                            "scene too large for the octree: the device builder overflowed at " +
-                                std::to_string(res.ref_overflow) +
-                                " references and the host builder would need about " +
-                                std::to_string(need >> 30) + " GiB; lower max_depth or raise "
-                                "leaf_capacity");
+            return fail(r, RT_E_NOMEM,
+                        "scene too large for the octree: the device builder overflowed at " +
+                            std::to_string(res.ref_overflow) +
+                            " references (a host build would need about " +
+                            std::to_string((res.ref_overflow * 64ull) >> 30) +
+                            " GiB); lower max_depth or raise leaf_capacity");
+        }
+        if (e == hipErrorOutOfMemory) {
+            // HBM cannot hold the device build's working set: build the
+            // identical tree on the host instead (rt_scene_info.builder then
+            // reports RT_BUILDER_HOST); build_octree refuses past 2^31
+            // references and reports host allocation failure as RT_E_NOMEM
+            (void)hipGetLastError();
             host = true;
         } else if (e != hipSuccess) {
             return hip_fail(r, e, "device octree build");
@@ -556,6 +595,32 @@ int mark_queued(rt_renderer* r, hipStream_t st) {
     return RT_OK;
 }
 
+// A frame the kernel found incomplete (its wave queue's bounded slot wait
+// gave up, rt_kernels.hip) stored its id in the renderer's pinned word; each
+// new value is reported once.  A plain host read: rt_render calls it before
+// every frame with no sync, rt_synchronize / rt_readback / stats frames after
+// theirs.
+int queue_report(rt_renderer* r) {
+    const uint32_t v = __atomic_load_n(r->qerr_host, __ATOMIC_ACQUIRE);
+    if (v == r->qerr_seen) return RT_OK;
+    r->qerr_seen = v;
+    return fail(r, RT_E_HIP, "scene kernel: wave-queue slot never published: frame " +
+                                 std::to_string(v) + " of this renderer is incomplete");
+}
+
+// RT_FLAG_TEST_POISON: the frame's outputs filled with a sentinel first
+// (rt.h), so a pixel no kernel writes shows in the readback.
+int poison_outputs(rt_renderer* r, const FrameArgs& a, hipStream_t st) {
+    if (!(r->cfg.flags & RT_FLAG_TEST_POISON)) return RT_OK;
+    const size_t px = a.tiles ? (size_t)a.n_tiles * a.tile_size * a.tile_size : (size_t)a.W * a.H;
+    RT_HIP(r, hipMemsetAsync(a.out8, 0xAB, px * 4, st));
+    // (the compat kernel writes RGBA8 only: no radiance to check there)
+    if (a.out32 && r->cfg.mode == RT_MODE_SCENE)
+        RT_HIP(r, hipMemsetAsync(a.out32, 0xFF, (size_t)a.W * a.H * 16, st));
+    if (a.accum && !a.accum_in) RT_HIP(r, hipMemsetAsync(a.accum, 0xFF, (size_t)a.W * a.H * 16, st));
+    return RT_OK;
+}
+
 int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : r->stream;
     if (r->cfg.mode == RT_MODE_SCENE && !r->has_scene)
@@ -640,7 +705,9 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     }
     a.counters = r->counters.p;
     RT_HIP(r, hipMemsetAsync(r->counters.p, 0, words * sizeof(unsigned long long), st));
+    if ((ost = poison_outputs(r, a, st))) return ost;
     a.count_work = stats ? 1u : 0u;
+    a.test_fault_queue = r->test_fault_queue && !stats ? 1u : 0u;
     if (stats) RT_HIP(r, hipEventRecord(r->ev0, st));
 #ifdef RT_TIMELINE
     // diagnostic build (tools/timeline.sh): every stats frame appends its
@@ -684,7 +751,6 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     }
 #endif
     if ((ost = mark_queued(r, st))) return ost;
-    r->check_queue = a.wq_slots != nullptr && !stats;
 #ifdef RT_TIMELINE
     if (tl_file) {
         std::vector<unsigned long long> h(tl_words);
@@ -715,11 +781,7 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
         stats->ms = ms;
         stats->samples_per_pixel = r->cfg.mode != RT_MODE_SCENE ? 1u
                                    : a.accum ? a.spp * r->frames_accum : a.spp;
-        unsigned long long qerr = 0;
-        RT_HIP(r, hipMemcpy(&qerr, r->counters.p + kWaveQueueClaim + 1, sizeof(qerr),
-                            hipMemcpyDeviceToHost));
-        if (qerr)
-            return fail(r, RT_E_HIP, "scene kernel: wave-queue slot never published (frame incomplete)");
+        if ((ost = queue_report(r))) return ost;
     }
     return RT_OK;
 }
@@ -798,8 +860,11 @@ int rt_create(const rt_config* cfg, rt_renderer** out) {
     r->device = dev;
     r->W = cfg->width;
     r->H = cfg->height;
-    if (const char* cd = getenv("RT_TEST_CLAIM_DELAY"))  // test only (tests/test_gpu_variants.py)
+    // test only (tests/test_gpu_variants.py, test_gpu_queue_report.py)
+    if (const char* cd = test_env(cfg->flags, "RT_TEST_CLAIM_DELAY"))
         r->test_claim_delay = static_cast<uint32_t>(std::min(100000ul, strtoul(cd, nullptr, 10)));
+    if (const char* fe = test_env(cfg->flags, "RT_TEST_FAULT"))
+        r->test_fault_queue = strcmp(fe, "queue:0") == 0;
     // src/renderer.cu:87-89: K0 = mat3(1000,0,640, 0,1000,340, 0,0,1), pose = mat4(1)
     const float K0[9] = {1000.f, 0.f, 640.f, 0.f, 1000.f, 340.f, 0.f, 0.f, 1.f};
     memcpy(r->K, K0, sizeof(K0));
@@ -811,6 +876,14 @@ int rt_create(const rt_config* cfg, rt_renderer** out) {
     if (e == hipSuccess) e = hipEventCreate(&r->ev0);
     if (e == hipSuccess) e = hipEventCreate(&r->ev1);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&r->done, hipEventDisableTiming);
+    // the frame-failure word: pinned, host-coherent, mapped for the kernels
+    if (e == hipSuccess)
+        e = hipHostMalloc(reinterpret_cast<void**>(&r->qerr_host), sizeof(uint32_t),
+                          hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) {
+        *r->qerr_host = 0;
+        e = hipHostGetDevicePointer(reinterpret_cast<void**>(&r->qerr_dev), r->qerr_host, 0);
+    }
     if (e != hipSuccess) {
         st = hip_fail(nullptr, e, "rt_create");
         rt_destroy(r);
@@ -864,6 +937,7 @@ int rt_destroy(rt_renderer* r) {
     if (r->ev1) (void)hipEventDestroy(r->ev1);
     if (r->done) (void)hipEventDestroy(r->done);
     if (r->stream) (void)hipStreamDestroy(r->stream);
+    if (r->qerr_host) (void)hipHostFree(r->qerr_host);
     delete r;
     return RT_OK;
 }
@@ -1062,6 +1136,14 @@ int rt_generate_spheres(uint32_t n, uint32_t seed, float* spheres_out, uint32_t*
 int rt_render(rt_renderer* r, void* dev_rgba8, void* stream, rt_stats* stats) {
     if (!r) return fail(r, RT_E_INVALID, "rt_render: null handle");
     int st;
+    // an earlier frame the kernel found incomplete: reported here, before
+    // anything is queued, by a host read (no sync: the Displayer's frames
+    // into a mapped PBO are never read back)
+    if (r->multi) {
+        if ((st = multi_queue_report(r))) return st;
+    } else if ((st = queue_report(r))) {
+        return st;
+    }
     if ((st = set_device(r))) return st;
     // (a multi-device handle's renderers accumulate per tile list, in multi_render)
     if (!r->multi) accum_pixels(r, nullptr, 0, 0);
@@ -1225,19 +1307,8 @@ int rt_reset_accumulation(rt_renderer* r) {
 }
 
 // After the renderer's work has completed: the wave queue's bounded wait
-// (rt_kernels.hip) flags a frame whose slot was never published instead of
-// hanging; report it for the last frame.
-static int check_last_frame(rt_renderer* r) {
-    if (!r->check_queue) return RT_OK;
-    r->check_queue = false;
-    unsigned long long qerr = 0;
-    RT_HIP(r, hipMemcpy(&qerr, r->counters.p + kWaveQueueClaim + 1, sizeof(qerr),
-                        hipMemcpyDeviceToHost));
-    if (qerr)
-        return fail(r, RT_E_HIP, "scene kernel: wave-queue slot never published (frame incomplete)");
-    return RT_OK;
-}
-
+// (rt_kernels.hip) marks a frame whose slot was never published instead of
+// hanging; every such frame not reported yet is reported now.
 int rt_synchronize(rt_renderer* r) {
     if (!r) return RT_E_INVALID;
     int st;
@@ -1245,7 +1316,7 @@ int rt_synchronize(rt_renderer* r) {
     if ((st = set_device(r))) return st;
     RT_HIP(r, hipStreamSynchronize(r->stream));
     if (r->pending) RT_HIP(r, hipEventSynchronize(r->done));
-    return check_last_frame(r);
+    return queue_report(r);
 }
 
 int rt_readback(rt_renderer* r, uint8_t* host_rgba8, float* host_rgba32f) {
@@ -1256,7 +1327,7 @@ int rt_readback(rt_renderer* r, uint8_t* host_rgba8, float* host_rgba32f) {
     // the frame may have been queued on a caller's stream
     RT_HIP(r, hipStreamSynchronize(r->stream));
     if (r->pending) RT_HIP(r, hipEventSynchronize(r->done));
-    if ((st = check_last_frame(r))) return st;
+    if ((st = queue_report(r))) return st;
     const size_t px = (size_t)r->W * r->H;
     if (host_rgba8) RT_HIP(r, hipMemcpy(host_rgba8, r->fb.p, px * 4, hipMemcpyDeviceToHost));
     if (host_rgba32f) {
@@ -1425,23 +1496,25 @@ int multi_wait(rt_renderer* r) {
     return RT_OK;
 }
 
-// multi_wait, then every device's check of its last frame (the wave queue's
-// bounded wait flags a frame whose slot was never published): a flagged
-// device's slab was gathered and unpacked incomplete, so the handle reports
-// RT_E_HIP naming that device, as a single-device renderer does for itself.
-int multi_synchronize(rt_renderer* r) {
-    int st;
-    if ((st = multi_wait(r))) return st;
+// Every device's failure word (queue_report): a device whose frame the wave
+// queue's bounded wait marked incomplete had its slab gathered and unpacked
+// incomplete, so the handle reports RT_E_HIP naming that device, as a
+// single-device renderer does for itself.  A host read, no sync.
+int multi_queue_report(rt_renderer* r) {
     MultiState& m = *r->multi;
     for (size_t k = 0; k < m.peers.size(); ++k) {
         rt_renderer* p = m.peers[k];
         if (!p) continue;
-        if ((st = set_device(p)) || (st = check_last_frame(p))) {
-            const std::string msg = p->err + peer_name(m, k);
-            (void)set_device(r);
-            return fail(r, st, msg);
-        }
+        if (const int st = queue_report(p)) return fail(r, st, p->err + peer_name(m, k));
     }
+    return RT_OK;
+}
+
+// multi_wait, then every device's failure word.
+int multi_synchronize(rt_renderer* r) {
+    int st;
+    if ((st = multi_wait(r))) return st;
+    if ((st = multi_queue_report(r))) return st;
     return set_device(r);
 }
 
@@ -1457,24 +1530,21 @@ int multi_render(rt_renderer* r, uint32_t* out, hipStream_t hs, rt_stats* stats)
     const uint32_t n = static_cast<uint32_t>(m.devs.size()), ts = MultiState::kTs;
     const int f = static_cast<int>(m.frame % MultiState::F);
     const auto t0 = std::chrono::steady_clock::now();
+    const bool timed = m.timing;
+    m.timed[f] = false;
     rt_stats sum{};
     // 1. every device renders its tiles into its slab of slot f
     for (uint32_t k = 0; k < n; ++k) {
         rt_renderer* p = m.peers[k];
         RT_HIP(r, hipSetDevice(m.devs[k]));
         if (m.used[f]) RT_HIP(r, hipStreamWaitEvent(p->stream, m.sent[f][k], 0));
-        RT_HIP(r, hipEventRecord(m.started[f][k], p->stream));
+        if (timed) RT_HIP(r, hipEventRecord(m.t_start[f][k], p->stream));
         rt_stats sk{};
         st = render_tiles_one(p, m.ids[k].data(), static_cast<uint32_t>(m.ids[k].size()), ts,
                               m.slab[f][k], p->stream, stats ? &sk : nullptr);
         if (st) {
             r->err = p->err + peer_name(m, k);
             return st;
-        }
-        if (m.fault == MultiState::kQueue && k == m.fault_k && !stats) {
-            // RT_TEST_FAULT=queue:k: the word the kernel's bounded slot wait
-            // sets (rt_kernels.hip), set after device k's render
-            RT_HIP(r, hipMemsetAsync(p->counters.p + kWaveQueueClaim + 1, 1, 1, p->stream));
         }
         if (stats) {
             sum.primary_rays += sk.primary_rays;
@@ -1483,6 +1553,7 @@ int multi_render(rt_renderer* r, uint32_t* out, hipStream_t hs, rt_stats* stats)
             sum.prims_tested += sk.prims_tested;
             sum.samples_per_pixel = sk.samples_per_pixel;
         }
+        if (timed) RT_HIP(r, hipEventRecord(m.t_end[f][k], p->stream));
         RT_HIP(r, hipEventRecord(m.rendered[f][k], p->stream));
         RT_HIP(r, hipStreamWaitEvent(m.cs[k], m.rendered[f][k], 0));
     }
@@ -1525,14 +1596,19 @@ int multi_render(rt_renderer* r, uint32_t* out, hipStream_t hs, rt_stats* stats)
     //    earlier work (a mapped display buffer is ready) and the slabs' arrival
     RT_HIP(r, hipSetDevice(m.devs[0]));
     RT_HIP(r, hipEventRecord(m.recvd[f], m.cs[0]));
+    // (RT_FLAG_TEST_POISON: the frame's pixels all come from the unpack)
+    if (r->cfg.flags & RT_FLAG_TEST_POISON)
+        RT_HIP(r, hipMemsetAsync(out, 0xAB, (size_t)r->W * r->H * 4, hs));
     RT_HIP(r, hipEventRecord(m.out_ready, hs));
     RT_HIP(r, hipStreamWaitEvent(m.cs[0], m.out_ready, 0));
     hipError_t e = launch_unpack(static_cast<const uint32_t*>(m.recv[f]), m.d_all_ids, n * m.S, ts,
                                  (r->W + ts - 1) / ts, r->W, r->H, out, m.cs[0]);
     if (e != hipSuccess) return hip_fail(r, e, "multi-device unpack");
+    if (timed) RT_HIP(r, hipEventRecord(m.t_unpacked[f], m.cs[0]));
     RT_HIP(r, hipEventRecord(m.unpacked[f], m.cs[0]));
     RT_HIP(r, hipStreamWaitEvent(hs, m.unpacked[f], 0));
     m.used[f] = true;
+    m.timed[f] = timed;
     ++m.frame;
     if (stats) {
         RT_HIP(r, hipStreamSynchronize(hs));
@@ -1610,9 +1686,8 @@ void multi_destroy(rt_renderer* r) {
         (void)hipSetDevice(m->devs[k]);
         for (int f = 0; f < MultiState::F; ++f) {
             if (k < m->slab[f].size() && m->slab[f][k]) (void)hipFree(m->slab[f][k]);
-            if (k < m->started[f].size() && m->started[f][k]) (void)hipEventDestroy(m->started[f][k]);
-            if (k < m->rendered[f].size() && m->rendered[f][k]) (void)hipEventDestroy(m->rendered[f][k]);
-            if (k < m->sent[f].size() && m->sent[f][k]) (void)hipEventDestroy(m->sent[f][k]);
+            for (auto* ev : {&m->rendered[f], &m->sent[f], &m->t_start[f], &m->t_end[f]})
+                if (k < ev->size() && (*ev)[k]) (void)hipEventDestroy((*ev)[k]);
         }
         if (k < m->comms.size() && m->comms[k]) (void)rccl_api().CommDestroy(m->comms[k]);
         if (k < m->cs.size() && m->cs[k]) (void)hipStreamDestroy(m->cs[k]);
@@ -1623,6 +1698,7 @@ void multi_destroy(rt_renderer* r) {
         if (m->recv[f]) (void)hipFree(m->recv[f]);
         if (m->recvd[f]) (void)hipEventDestroy(m->recvd[f]);
         if (m->unpacked[f]) (void)hipEventDestroy(m->unpacked[f]);
+        if (m->t_unpacked[f]) (void)hipEventDestroy(m->t_unpacked[f]);
     }
     if (m->out) (void)hipStreamDestroy(m->out);
     if (m->out_ready) (void)hipEventDestroy(m->out_ready);
@@ -1660,10 +1736,10 @@ int rt_create_multi(const rt_config* cfg, const int32_t* devices, uint32_t n_dev
     if (cfg->flags & RT_FLAG_RADIANCE)
         return fail(nullptr, RT_E_INVALID,
                     "rt_create_multi: RT_FLAG_RADIANCE is not supported on a multi-device handle");
-    // test-only fault injection (MultiState::Fault)
+    // test-only fault injection (MultiState::Fault, RT_FLAG_TEST_HOOKS)
     int fault = MultiState::kNone;
     uint32_t fault_k = 0;
-    if (const char* fe = getenv("RT_TEST_FAULT")) {
+    if (const char* fe = test_env(cfg->flags, "RT_TEST_FAULT")) {
         const std::string f(fe);
         const size_t c = f.find(':');
         const std::string kind = f.substr(0, c);
@@ -1692,9 +1768,10 @@ int rt_create_multi(const rt_config* cfg, const int32_t* devices, uint32_t n_dev
     m->cs.assign(n_devices, nullptr);
     for (int f = 0; f < MultiState::F; ++f) {
         m->slab[f].assign(n_devices, nullptr);
-        m->started[f].assign(n_devices, nullptr);
         m->rendered[f].assign(n_devices, nullptr);
         m->sent[f].assign(n_devices, nullptr);
+        m->t_start[f].assign(n_devices, nullptr);
+        m->t_end[f].assign(n_devices, nullptr);
     }
     auto bail = [&](int code) {
         g_last_error = r->err.empty() ? g_last_error : r->err;
@@ -1712,14 +1789,19 @@ int rt_create_multi(const rt_config* cfg, const int32_t* devices, uint32_t n_dev
             return bail(st);
         }
     }
+    // RT_TEST_FAULT=queue:k: peer k's plain frames report themselves failed
+    // (rt_create honoured a "queue:0" on every peer: only peer k keeps it)
+    for (uint32_t k = 0; k < n_devices; ++k)
+        m->peers[k]->test_fault_queue = m->fault == MultiState::kQueue && k == m->fault_k;
     for (uint32_t k = 0; k < n_devices; ++k) {
         hipError_t e = hipSetDevice(devices[k]);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&m->cs[k], hipStreamNonBlocking);
         for (int f = 0; f < MultiState::F && e == hipSuccess; ++f) {
-            // started / rendered time device k's render (rt_get_multi_timing)
-            e = hipEventCreate(&m->started[f][k]);
-            if (e == hipSuccess) e = hipEventCreate(&m->rendered[f][k]);
+            e = hipEventCreateWithFlags(&m->rendered[f][k], hipEventDisableTiming);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&m->sent[f][k], hipEventDisableTiming);
+            // t_start / t_end time device k's render (rt_get_multi_timing)
+            if (e == hipSuccess) e = hipEventCreate(&m->t_start[f][k]);
+            if (e == hipSuccess) e = hipEventCreate(&m->t_end[f][k]);
         }
         if (e != hipSuccess)
             return bail(hip_fail(r, e, ("rt_create_multi: streams/events" + peer_name(*m, k)).c_str()));
@@ -1737,7 +1819,8 @@ int rt_create_multi(const rt_config* cfg, const int32_t* devices, uint32_t n_dev
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&m->out, hipStreamNonBlocking);
         for (int f = 0; f < MultiState::F && e == hipSuccess; ++f) {
             e = hipEventCreateWithFlags(&m->recvd[f], hipEventDisableTiming);
-            if (e == hipSuccess) e = hipEventCreate(&m->unpacked[f]);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&m->unpacked[f], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreate(&m->t_unpacked[f]);
         }
         if (e == hipSuccess) e = hipEventCreateWithFlags(&m->out_ready, hipEventDisableTiming);
         if (e != hipSuccess) return bail(hip_fail(r, e, "rt_create_multi: events"));
@@ -1766,19 +1849,27 @@ int rt_get_multi_timing(rt_renderer* r, rt_multi_timing* t) {
     if (!r || !t) return fail(r, RT_E_INVALID, "rt_get_multi_timing: null argument");
     if (!r->multi) return fail(r, RT_E_STATE, "rt_get_multi_timing: not a multi-device handle");
     MultiState& m = *r->multi;
+    // from now on frames record their timing events
+    const bool was_on = m.timing;
+    m.timing = true;
     if (!m.frame) return fail(r, RT_E_STATE, "rt_get_multi_timing: no frame rendered yet");
+    const int f = static_cast<int>((m.frame - 1) % MultiState::F);
+    if (!m.timed[f])
+        return fail(r, RT_E_STATE,
+                    was_on ? "rt_get_multi_timing: the last frame was not timed"
+                           : "rt_get_multi_timing: timing starts with the next frame (frames "
+                             "record timing events once it has been asked for)");
     int st;
     if ((st = multi_wait(r))) return st;
     memset(t, 0, sizeof(*t));
-    const int f = static_cast<int>((m.frame - 1) % MultiState::F);
     t->n_devices = static_cast<uint32_t>(m.devs.size());
     t->frame = m.frame - 1;
     for (size_t k = 0; k < m.devs.size(); ++k) {
         RT_HIP(r, hipSetDevice(m.devs[k]));
-        RT_HIP(r, hipEventElapsedTime(&t->render_ms[k], m.started[f][k], m.rendered[f][k]));
+        RT_HIP(r, hipEventElapsedTime(&t->render_ms[k], m.t_start[f][k], m.t_end[f][k]));
     }
     RT_HIP(r, hipSetDevice(m.devs[0]));
-    RT_HIP(r, hipEventElapsedTime(&t->deliver_ms, m.rendered[f][0], m.unpacked[f]));
+    RT_HIP(r, hipEventElapsedTime(&t->deliver_ms, m.t_end[f][0], m.t_unpacked[f]));
     return RT_OK;
 }
 

@@ -8,7 +8,7 @@
 //   rt_cli [--config c1|c2|c3|c4|c5] [--width W --height H --spp S --spheres N
 //           --depth D] [--frames F] [--out image.ppm] [--scene in.rtsph]
 //          [--save-scene out.rtsph] [--host-build] [--gpus N [--same-device]]
-//          [--progressive] [--panel] [--walk]
+//          [--progressive] [--panel] [--walk] [--test-poison]
 //
 // --panel prints the stats panel (rt_camera.hpp StatsPanel: the reference's
 // ImGui window numbers plus Mrays/s, spp, GPUs) after every frame; --walk
@@ -106,7 +106,7 @@ int run_multi(const rt_config& rc, const float pose[16], int gpus, bool same_dev
 int main(int argc, char** argv) {
     std::string cfg = "c2", out, scene_in, scene_out;
     bool host_build = false, same_device = false, progressive = false, panel = false,
-         walk = false;
+         walk = false, poison = false;
     int gpus = 1;
     bool multi = false;  // --gpus given (even 1: a 1-device RCCL communicator)
     int W = 0, H = 0, spp = 0, frames = 3;
@@ -136,6 +136,7 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--progressive")) progressive = true;
         else if (!strcmp(argv[i], "--panel")) panel = true;
         else if (!strcmp(argv[i], "--walk")) walk = true;
+        else if (!strcmp(argv[i], "--test-poison")) poison = true;  // RT_FLAG_TEST_POISON (tests)
         else {
             fprintf(stderr, "unknown argument %s\n", argv[i]);
             return 2;
@@ -168,6 +169,7 @@ int main(int argc, char** argv) {
         rc.mode = c->mode;
         if (host_build) rc.flags |= RT_FLAG_HOST_BUILD;
         if (progressive) rc.flags |= RT_FLAG_PROGRESSIVE;
+        if (poison) rc.flags |= RT_FLAG_TEST_POISON;
         rtamd::KernelRenderer r(rc);
         r.resize(W, H);
         // Displayer default orientation (include/window/displayer.h:47-52):

@@ -226,6 +226,14 @@ __device__ __forceinline__ KernArgs* kernargs() {
     return p;
 }
 
+// An incomplete frame (FrameArgs::qerr): this frame's id into the renderer's
+// pinned host word, a plain system-scope store (no atomic over the host
+// link), visible to the host without a copy.  Called by a wave's lead lane.
+__device__ __forceinline__ void frame_failed() {
+    KernArgs* ka = kernargs();
+    __hip_atomic_store(ka->qerr, ka->frame_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 constexpr uint32_t kSortMaxRounds = 4;  // up to 256 samples per pixel
 constexpr uint32_t kSortMax = 64u * kSortMaxRounds;
 // per wave: per sample a slot {t, sphere} -> {lam | miss g, albedo | miss b}
@@ -282,6 +290,49 @@ __device__ __forceinline__ uint32_t leaf_buf_base(const SceneArgs& S, bool sorte
     return head + wave * kLeafBuf;
 }
 
+// LDS leaf staging by gfx950's direct global -> LDS load (RT_GLDS, VERDICT r05
+// item 5): ONE global_load_lds_dwordx4 writes spheres 0 .. cnt - 1 of the leaf
+// at src into dst[0 .. cnt - 1] without a VGPR round trip or a ds_write.  Its
+// LDS destination is M0 + 16 x lane id, so lane k must fetch sphere k: the
+// instruction runs with exec = lanes 0 .. cnt - 1 (cnt <= kLeafBuf = 32),
+// whichever of them are active in the walk (an inactive lane's sphere is
+// still in the leaf, its fetch in bounds), and the address is computed under
+// that exec too.  M0 and exec are restored in the same statement.  The load
+// is invisible to the compiler's waitcnt bookkeeping: the explicit vmcnt(0)
+// retires it before the chunks' ds_reads (the issuing wave is the reader, so
+// no barrier is needed; MI355X_MICROARCH.md item 7).
+#ifndef RT_GLDS
+#define RT_GLDS 0
+#endif
+__device__ __forceinline__ void glds_leaf(const float4* src, float4* dst, uint32_t cnt) {
+    typedef __attribute__((address_space(3))) float4 LdsF4;
+    const uint32_t lds = __builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(reinterpret_cast<uintptr_t>((LdsF4*)dst)));
+    const uint64_t base = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(
+                               static_cast<uint32_t>(reinterpret_cast<uint64_t>(src) >> 32)))
+                           << 32) |
+                          __builtin_amdgcn_readfirstlane(
+                              static_cast<uint32_t>(reinterpret_cast<uint64_t>(src)));
+    const uint64_t mask = (1ull << cnt) - 1ull;
+    uint64_t save;
+    uint32_t keep, off;
+    asm volatile(
+        "s_mov_b64 %[save], exec\n\t"
+        "s_mov_b64 exec, %[mask]\n\t"
+        "v_mbcnt_lo_u32_b32 %[off], -1, 0\n\t"
+        "v_lshlrev_b32 %[off], 4, %[off]\n\t"
+        "s_mov_b32 %[keep], m0\n\t"
+        "s_mov_b32 m0, %[lds]\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %[off], %[base]\n\t"
+        "s_mov_b32 m0, %[keep]\n\t"
+        "s_mov_b64 exec, %[save]\n\t"
+        "s_waitcnt vmcnt(0)"
+        : [save] "=&s"(save), [keep] "=&s"(keep), [off] "=&v"(off)
+        : [mask] "s"(mask), [lds] "s"(lds), [base] "s"(base)
+        : "memory");
+}
+
 // Grid-space octree walk (DESIGN.md "Octree walk"): mirrored origin so every
 // direction component is >= 0 (the Revelles entry step of hit_sphere,
 // src/renderer.cu:23-43), cell planes at integer grid coordinates, descend by
@@ -290,13 +341,19 @@ __device__ __forceinline__ uint32_t leaf_buf_base(const SceneArgs& S, bool sorte
 // The per-thread ancestor stack lives in LDS, [depth-1][thread] (conflict-free).
 // kAnyHit: compile-time any-hit; with kDynAny the mode comes from `any_rt`
 // instead, so ONE inlined walk serves both the primary and the shadow ray.
+// kShadowL: this walk's any-hit rays are the frame's shadow rays, whose
+// direction is FrameArgs::L in every lane: only then may it use
+// the light-plane screen and keep its reciprocals wave-uniform.  Any other
+// any-hit walk (a per-lane direction: ambient occlusion, area lights) keeps
+// the full discriminant screen.
 template <bool kAnyHitT, int kChunk = 2, bool kDynAny = false, bool kStats = true,
-          bool kNoStack = false>
+          bool kNoStack = false, bool kShadowL = false>
 __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, float o2, float d0,
                                      float d1, float d2, float tmin, float tmax, float& tout,
                                      uint32_t& iout, uint32_t& n_nodes, uint32_t& n_prims,
                                      uint2* __restrict__ stk, bool any_rt = false,
                                      uint32_t* bs = nullptr) {
+    static_assert(!kShadowL || kAnyHitT || kDynAny, "a shadow walk along L is an any-hit walk");
     const bool kAnyHit = kDynAny ? any_rt : kAnyHitT;
     const uint32_t D = S.max_depth;
     const uint32_t G = 1u << D;
@@ -319,7 +376,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
 #else
     constexpr bool kShdOk = true;
 #endif
-    const bool shd = kShdOk && kAnyHit;  // every any-hit walk is a shadow ray along L
+    const bool shd = kShdOk && kShadowL && kAnyHit;  // a shadow ray along L (the caller says so)
     float up = 0.0f, vp = 0.0f;
     if (shd) {
         KernArgs* ke = kernargs();
@@ -348,7 +405,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         inv[i] = 1.0f / (a * S.scale[i]);
         // a shadow walk's direction is the frame's light direction, the same
         // in every lane (sample_color_unified): its reciprocals live in SGPRs
-        if (kAnyHitT && !kDynAny)
+        if (kShadowL && kAnyHitT && !kDynAny)
             inv[i] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
                                                    __builtin_bit_cast(uint32_t, inv[i])));
         nog[i] = -(og * inv[i]);
@@ -512,9 +569,13 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             extern __shared__ __attribute__((aligned(16))) float4 lds_leaf[];
             const uint32_t lb = leaf_buf_base(S, kNoStack);
             const float4* __restrict__ pu = prim_sp + off_u;
+#if RT_GLDS
+            glds_leaf(pu, lds_leaf + lb, cnt_u);
+#else
             const uint64_t act = __ballot(1);
             const uint32_t na = static_cast<uint32_t>(__popcll(act));
             for (uint32_t k = lane_rank(act); k < cnt_u; k += na) lds_leaf[lb + k] = pu[k];
+#endif
             // (a wave's LDS operations complete in order: the reads below see
             // the writes, and the compiler keeps them in order: same array)
             return chunks([&](uint32_t k) { return lds_leaf[lb + k]; }, off_u, cnt_u);
@@ -799,9 +860,9 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
                 // lane: read afresh from the kernel arguments (SGPRs), not the
                 // lanes' d registers
                 KernArgs* kl = kernargs();
-                hit = walk<true, kChunk, false, kStats>(S, r0, r1, r2, kl->L[0], kl->L[1], kl->L[2],
-                                                        0.0f, INFINITY, t, idx, n_nodes, n_prims,
-                                                        static_cast<uint2*>(stk), true, bs);
+                hit = walk<true, kChunk, false, kStats, false, true>(
+                    S, r0, r1, r2, kl->L[0], kl->L[1], kl->L[2], 0.0f, INFINITY, t, idx, n_nodes,
+                    n_prims, static_cast<uint2*>(stk), true, bs);
             }
         }
         if (phase == 0) {
@@ -1113,9 +1174,9 @@ __device__ __forceinline__ void shade_pixel_sorted(const FrameArgs& a, float* wl
             KernArgs* kl = kernargs();
             float ts;
             uint32_t is;
-            occ = walk<false, kChunk, true, kStats, true>(S, o0, o1, o2, kl->L[0], kl->L[1], kl->L[2],
-                                                          0.0f, INFINITY, ts, is, n_nodes, n_prims,
-                                                          static_cast<uint2*>(stk), true, bs);
+            occ = walk<false, kChunk, true, kStats, true, true>(
+                S, o0, o1, o2, kl->L[0], kl->L[1], kl->L[2], 0.0f, INFINITY, ts, is, n_nodes,
+                n_prims, static_cast<uint2*>(stk), true, bs);
         }
         if (has) {
             RT_BS(kBsShadeLoad);
@@ -1293,8 +1354,11 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
             if (lead && (u0 == 0u || (w0 <= half && half < w0 + chunk))) {
                 // (test only: hold XCD 0's first claim back until the other
                 // claims of its first slots would have been taken)
-                if (q == 0u && u0 == 0u)
+                if (q == 0u && u0 == 0u) {
                     for (uint32_t d = kernargs()->wq_claim_delay; d; --d) __builtin_amdgcn_s_sleep(127);
+                    // (test only, RT_TEST_FAULT=queue:k: report this frame as failed)
+                    if (kernargs()->test_fault_queue) frame_failed();
+                }
                 const uint32_t slot = u0 == 0u ? 0u : s + 1u;
                 const uint32_t g = static_cast<uint32_t>(atomicAdd(claims, 1ull));
                 if (slot < a.wq_slot_stride)
@@ -1313,7 +1377,7 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
                         e = __hip_atomic_load(slots + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         if (e != 0u) break;
                         if (spin == (1u << 22)) {
-                            atomicOr(a.counters + kWaveQueueClaim + 1, 1ull);
+                            frame_failed();
                             e = kSlotNone;
                             break;
                         }
@@ -1321,7 +1385,10 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
                     }
                 }
                 e = __builtin_amdgcn_readfirstlane(e);
+#ifndef RT_TEST_CLAIM_RULE_R4  // (test-only build of round 4's rule: the negative
+                               // control of tests/test_gpu_queue_report.py)
                 if (e == kSlotNone && s < owed) continue;  // a slot this wave claimed is ahead
+#endif
             }
             if (s != cached_s) {
 #ifdef RT_TIMELINE

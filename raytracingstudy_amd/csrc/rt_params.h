@@ -29,8 +29,8 @@ constexpr uint32_t kVariantWaveQLow = 4;   // the per-wave queue for spp < 8 too
 constexpr uint32_t kPrimPad = 4;
 
 // A/B toggles (rt_config.flags bits 20..27), results identical either way
-constexpr uint32_t kOptDeviceBuildRefuse = 1u << 0;  // bit 0: treat every tree as too large for
-                                                     // the device builder (tests its host fallback)
+constexpr uint32_t kOptDeviceBuildRefuse = 1u << 0;  // bit 0: the device build reports running out
+                                                     // of HBM (tests its host fallback)
 constexpr uint32_t kOptBtsShift = 1;       // bits 1..3: force the block-tile side (A/B):
                                            // 0 auto, 1 = 16, 2 = 8, 3 = 4, 4 = 2 pixels
 constexpr uint32_t kOptNoWgCap = 1u << 7; // bit 7: 1-spp frames without the 3-workgroups-per-CU cap
@@ -52,7 +52,7 @@ constexpr uint32_t kCellTableMaxK = 7;        // 2^21 entries, 16 MiB
 constexpr uint32_t kCellTableAuto = 0xFFFFFFFFu;
 constexpr uint32_t kCellTableOff = 0;
 
-// counters[] layout: [0..3] stats, [kQueueSlot] block-tile queue head (own
+// counters[] layout: [0..7] unused, [kQueueSlot] block-tile queue head (own
 // cache line), then 8 per-XCD wave-queue heads, one per 128-byte line
 constexpr uint32_t kQueueSlot = 8;
 constexpr uint32_t kWaveQueueBase = 16;
@@ -256,6 +256,15 @@ struct FrameArgs {
     uint32_t wq_slot_shift;    //   slot = 2^shift wave tiles: 12 a superblock, 6 one 8x8 block
     uint32_t wq_claim_delay;   // test only (RT_TEST_CLAIM_DELAY): XCD 0's ticket-0 wave sleeps
                                //   this many s_sleep 127 before claiming slot 0; 0 in product
+    // Wave-queue failure report: a wave whose slot was never published (the
+    // bounded wait below gave up) stores frame_id into this word of pinned,
+    // host-coherent memory (rt_renderer::qerr_host), which the host reads
+    // without a copy or a sync: the next rt_render reports it (the Displayer
+    // never reads back, src/window/displayer.cpp:51-53), as do rt_synchronize,
+    // rt_readback and stats frames.
+    uint32_t* qerr;
+    uint32_t frame_id;         // nonzero, per renderer
+    uint32_t test_fault_queue; // test only (RT_TEST_FAULT=queue:k): the frame reports itself failed
 #ifdef RT_TIMELINE
     unsigned long long* timeline;  // diagnostic build: 4 words per wave
 #endif

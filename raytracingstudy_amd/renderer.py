@@ -148,7 +148,7 @@ class KernelRenderer:
             if not 1 <= ct <= 15:
                 raise ValueError("cell_table must be None, 0 (off) or a depth 1..7")
             flags |= ct << _lib.RT_FLAG_CELL_TABLE_SHIFT
-        cfg.flags = flags
+        cfg.flags = flags | _lib.test_flags
         for i in range(3):
             cfg.light_dir[i] = float(light_dir[i])
         cfg.ambient = float(ambient)

@@ -17,6 +17,12 @@ def pytest_collection_modifyitems(session, config, items):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
+    # every renderer the suite makes fills its outputs
+    # with a sentinel before each frame (RT_FLAG_TEST_POISON), so a pixel the
+    # kernels skip can never hide behind a previous frame's identical image;
+    # and the RT_TEST_* hooks some tests set are honoured (RT_FLAG_TEST_HOOKS).
+    from raytracingstudy_amd import _lib
+    _lib.test_flags = _lib.RT_FLAG_TEST_HOOKS | _lib.RT_FLAG_TEST_POISON
 
 
 @pytest.fixture(scope="session")

@@ -761,10 +761,12 @@ def test_tree_past_the_builders_limits_is_refused_quickly(gpu, oracle):
 
 
 def test_device_build_falls_back_to_host_build(gpu, oracle):
-    """When the device builder refuses a tree (its per-level reference slots are
-    32-bit), rt_set_scene builds the identical tree on the host instead of
-    failing (forced here by the A/B bit kOptDeviceBuildRefuse): the scene
-    renders exactly like the oracle's."""
+    """When the device build runs out of HBM, rt_set_scene builds the
+    identical tree on the host instead of failing (forced here by the A/B bit
+    kOptDeviceBuildRefuse, which makes the device build report
+    hipErrorOutOfMemory; a 32-bit slot overflow is refused outright,
+    test_tree_past_the_builders_limits_is_refused_quickly): the scene renders
+    exactly like the oracle's."""
     c = _fuzz_case(26)
     with rt.KernelRenderer(c["w"], c["h"], mode="scene", spp=c["spp"], radiance=True,
                            shadows=c["shadows"], jitter=c["jitter"], light_dir=c["light"],

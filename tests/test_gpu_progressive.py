@@ -6,11 +6,17 @@ bit-identical to the oracle's progressive frame (orc_render_scene_frame), and
 K frames of 64 spp equal one 64*K-spp frame.  Accumulation restarts whenever
 what the pixels show changes (pose, intrinsic, size, scene, tile list).
 """
+import os
+import sys
+
 import numpy as np
 import pytest
 
 import raytracingstudy_amd as rt
 from raytracingstudy_amd.camera import display_pose, scene_pose
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import variant_check as vc  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -108,6 +114,7 @@ def test_progressive_tiles_match_full_frame(gpu, spheres):
             full.render()
             st = tiled.render_tiles(ids, ts, packed.data_ptr(), stats=True)
             assert st.samples_per_pixel == 4 * (k + 1)
+        vc.poison(tiled.framebuffer_ptr(), W * H * 4)  # a skipped tile shows
         tiled.unpack_tiles(packed.data_ptr(), ids, ts)
         assert np.array_equal(tiled.readback(), full.readback())
         # another tile list is another pixel set: starts over

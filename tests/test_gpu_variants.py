@@ -181,6 +181,7 @@ def test_sorted_rounds_match_oracle(gpu, oracle, n, w, h, spp, jitter, tiles):
             assert hip.hipMalloc(ctypes.byref(buf), ctypes.c_size_t(len(ids) * 64 * 64 * 4)) == 0
             try:
                 r.render_tiles(ids, 64, buf.value)
+                vc.poison(r.framebuffer_ptr(), w * h * 4)  # the fb holds img: hide nothing
                 r.unpack_tiles(buf.value, ids, 64)
                 assert np.array_equal(r.readback(), img)
             finally:

@@ -7,6 +7,9 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CLI = os.path.join(ROOT, "raytracingstudy_amd", "rt_cli")
+# every frame starts from a sentinel-filled framebuffer (RT_FLAG_TEST_POISON,
+# VERDICT r05 item 1), as in the Python tests (tests/conftest.py)
+POISON = "--test-poison"
 
 
 def test_cli_built():
@@ -21,7 +24,7 @@ def test_cli_fails_loudly_on_bad_args():
 @pytest.mark.gpu
 def test_cli_compat_ppm_matches_known_answers(gpu, tmp_path):
     out = tmp_path / "c1.ppm"
-    r = subprocess.run([CLI, "--config", "c1", "--frames", "1", "--out", str(out)],
+    r = subprocess.run([CLI, "--config", "c1", "--frames", "1", "--out", str(out), POISON],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     data = out.read_bytes()
@@ -35,7 +38,7 @@ def test_cli_compat_ppm_matches_known_answers(gpu, tmp_path):
 
 @pytest.mark.gpu
 def test_cli_scene_runs(gpu):
-    r = subprocess.run([CLI, "--config", "c2", "--frames", "2"], capture_output=True, text=True,
+    r = subprocess.run([CLI, "--config", "c2", "--frames", "2", POISON], capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0, r.stderr
     assert "Mrays/s" in r.stdout
@@ -49,7 +52,7 @@ def test_cli_scene_file_roundtrip_and_builders(gpu, tmp_path):
     for extra in (["--save-scene", str(f)], ["--scene", str(f)], ["--scene", str(f), "--host-build"]):
         o = tmp_path / ("img%d.ppm" % len(outs))
         r = subprocess.run([CLI, "--config", "c2", "--spheres", "3000", "--width", "160",
-                            "--height", "120", "--frames", "1", "--out", str(o), *extra],
+                            "--height", "120", "--frames", "1", "--out", str(o), POISON, *extra],
                            capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr
         assert ("host build" if "--host-build" in extra else "device build") in r.stdout
@@ -66,7 +69,7 @@ def test_cli_multi_renderer_frame_equals_single(gpu, tmp_path, gpus, same):
     (peer-copy transport), and as a 1-device RCCL communicator: the assembled
     frame equals the single-renderer frame byte for byte."""
     base = [CLI, "--config", "c3", "--spheres", "20000", "--width", "200", "--height", "150",
-            "--spp", "8", "--frames", "2"]
+            "--spp", "8", "--frames", "2", POISON]
     one, many = tmp_path / "one.ppm", tmp_path / "many.ppm"
     r1 = subprocess.run(base + ["--out", str(one)], capture_output=True, text=True, timeout=120)
     assert r1.returncode == 0, r1.stderr
@@ -83,7 +86,7 @@ def test_cli_panel_progressive_and_walk(gpu):
     """The stats panel (rt_camera.hpp) through the native driver: progressive
     frames accumulate spp while the camera stays put; walking restarts it."""
     base = [CLI, "--config", "c3", "--spheres", "20000", "--width", "160", "--height", "120",
-            "--spp", "4", "--frames", "3", "--panel", "--progressive"]
+            "--spp", "4", "--frames", "3", "--panel", "--progressive", POISON]
     r = subprocess.run(base, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     spp = [int(l.split()[1]) for l in r.stdout.splitlines() if l.startswith("spp ")]

@@ -39,6 +39,16 @@ CASES = [  # n, w, h, spp, depth
 ]
 
 
+def poison(dev_ptr: int, nbytes: int) -> None:
+    """Fill a device buffer with the 0xAB sentinel (the RT_FLAG_TEST_POISON
+    pattern) before a call that writes only part of it, e.g. rt_unpack_tiles:
+    a tile it skips then shows instead of the previous frame's pixels."""
+    import ctypes
+    hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
+    assert hip.hipMemset(ctypes.c_void_p(dev_ptr), 0xAB, ctypes.c_size_t(nbytes)) == 0
+    assert hip.hipDeviceSynchronize() == 0
+
+
 def diff_report(img, rad, st, ref) -> dict:
     """Which outputs differ from the oracle's, and how (empty dict: none)."""
     r8, r32, cnt = ref
