@@ -155,6 +155,10 @@ struct rt_renderer {
     uint32_t n_spheres = 0;
     std::vector<float> spheres;
     bool host_copy = false;
+    // leaf-reference arrays' length (prim_sp / prim_idx / the screen records):
+    // info.n_prim_refs, plus the gaps of the line-packed layout (pack_leaf_lines)
+    uint32_t prim_slots = 0;
+    bool leaf_packed = false;
     // test only: RT_TEST_CLAIM_DELAY at rt_create with RT_FLAG_TEST_HOOKS
     // (FrameArgs::wq_claim_delay)
     uint32_t test_claim_delay = 0;
@@ -312,6 +316,15 @@ void fill_frame_args(rt_renderer* r, FrameArgs& a) {
     a.variant = v ? v : (a.spp >= 8u ? kVariantWaveQ : kVariantWaveQLow);
 }
 
+// An A/B switch read from the environment ("0" off, anything else on), or dflt.
+bool env_flag(const char* name, bool dflt) {
+    const char* v = getenv(name);
+    return v && *v ? atoi(v) != 0 : dflt;
+}
+#ifndef RT_LEAF_PACK_DEFAULT
+#define RT_LEAF_PACK_DEFAULT 0
+#endif
+
 // A test hook's environment variable (RT_TEST_*): its value when the config
 // carries RT_FLAG_TEST_HOOKS, else NULL.  Either way a set variable is named
 // on stderr once per process, so a stray one is visible.
@@ -332,6 +345,82 @@ const char* test_env(uint32_t flags, const char* name) {
         }
     }
     return on ? v : nullptr;
+}
+
+// Leaf records of a breadth-first tree: a record's kind is in
+// its parent's leaf mask, and children come after their parent, so one
+// forward pass over the records finds them all.  Returned in record order.
+std::vector<uint32_t> leaf_records(const std::vector<uint2>& nodes) {
+    std::vector<uint8_t> internal(nodes.size(), 0);
+    std::vector<uint32_t> leaves;
+    if (!nodes.empty()) internal[0] = 1;  // (callers skip a root leaf)
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        if (!internal[i]) continue;
+        const uint32_t valid = nodes[i].y & 0xFFu, leafm = (nodes[i].y >> 8) & 0xFFu;
+        uint32_t k = nodes[i].x;
+        for (uint32_t c = 0; c < 8; ++c) {
+            if (!((valid >> c) & 1u)) continue;
+            if ((leafm >> c) & 1u) leaves.push_back(k);
+            else internal[k] = 1;
+            ++k;
+        }
+    }
+    std::sort(leaves.begin(), leaves.end(), [&](uint32_t a, uint32_t b) { return nodes[a].x < nodes[b].x; });
+    return leaves;
+}
+
+// Line-packed leaf lists: the builders store the leaf
+// lists back to back, so a leaf of n spheres (16 B each) straddles a 128-byte
+// cache line whenever it does not fit in the rest of one: 1.44-1.57 lines per
+// leaf on C3 / C5 / C5d against 1.05-1.12 when no leaf that fits a line
+// crosses one.  This relays the lists out so that it never does: a leaf whose
+// footprint (n, plus the slot past its end that a two-sphere chunk reads when
+// n is odd) fits in 8 slots starts in the current line if it fits there, else
+// at the next line; a longer leaf starts at a line.  The gaps hold what the
+// kPrimPad tail holds (zero spheres, or the test-only pad-fill spheres);
+// leaf records point at the new offsets; images and counters are unchanged
+// (the layout is not part of the spec).  The arrays grow by ~1.28x.
+int pack_leaf_lines(rt_renderer* r, SceneArgs& sc, rt_scene_info& in, const float4& pad) {
+    const size_t nn = in.n_nodes, np = in.n_prim_refs;
+    std::vector<uint2> nodes(nn);
+    RT_HIP(r, hipMemcpy(nodes.data(), sc.nodes, nn * sizeof(uint2), hipMemcpyDeviceToHost));
+    const std::vector<uint32_t> leaves = leaf_records(nodes);
+    std::vector<uint32_t> nf(leaves.size());
+    uint64_t off = 0;
+    for (size_t i = 0; i < leaves.size(); ++i) {
+        const uint32_t n = nodes[leaves[i]].y, f = n + (n & 1u), w = static_cast<uint32_t>(off & 7u);
+        if (w && (f > 8u || w + f > 8u)) off += 8u - w;
+        nf[i] = static_cast<uint32_t>(off);
+        off += n;
+    }
+    if (off + kPrimPad >= (uint64_t(1) << 32)) return RT_OK;  // (keep the compact layout)
+    const uint32_t slots = static_cast<uint32_t>(off);
+    std::vector<float4> sp(np), spn(slots, pad);
+    std::vector<uint32_t> ix(np), ixn(slots, 0u);
+    if (np) {
+        RT_HIP(r, hipMemcpy(sp.data(), sc.prim_sp, np * sizeof(float4), hipMemcpyDeviceToHost));
+        RT_HIP(r, hipMemcpy(ix.data(), sc.prim_idx, np * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    }
+    for (size_t i = 0; i < leaves.size(); ++i) {
+        uint2& rec = nodes[leaves[i]];
+        std::copy(sp.begin() + rec.x, sp.begin() + rec.x + rec.y, spn.begin() + nf[i]);
+        std::copy(ix.begin() + rec.x, ix.begin() + rec.x + rec.y, ixn.begin() + nf[i]);
+        rec.x = nf[i];
+    }
+    int st;
+    if ((st = ensure(r, r->d_prim_sp, (size_t)slots + kPrimPad))) return st;
+    if ((st = ensure(r, r->d_prim_idx, slots))) return st;
+    if (slots) {
+        RT_HIP(r, hipMemcpy(r->d_prim_sp.p, spn.data(), slots * sizeof(float4), hipMemcpyHostToDevice));
+        RT_HIP(r, hipMemcpy(r->d_prim_idx.p, ixn.data(), slots * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
+    RT_HIP(r, hipMemcpy(const_cast<uint2*>(sc.nodes), nodes.data(), nn * sizeof(uint2),
+                        hipMemcpyHostToDevice));
+    sc.prim_sp = r->d_prim_sp.p;
+    sc.prim_idx = r->d_prim_idx.p;
+    r->prim_slots = slots;
+    r->leaf_packed = true;
+    return RT_OK;
 }
 
 // Build the octree of the device sphere list (d_spheres) and point the
@@ -457,19 +546,24 @@ int build_scene(rt_renderer* r) {
         // pass the screen (NaN, or one covering the root box) to prove the
         // images and counters do not depend on the tail.
         const uint32_t mode = (r->cfg.flags >> RT_FLAG_PAD_FILL_SHIFT) & 3u;
-        float4 pad[kPrimPad];
-        for (uint32_t i = 0; i < kPrimPad; ++i) {
-            if (mode == 1) {
-                pad[i] = make_float4(NAN, NAN, NAN, NAN);
-            } else if (mode == 2) {
-                const float c = 0.5f * (rmin[0] + rmax[0]);
-                pad[i] = make_float4(c, 0.5f * (rmin[1] + rmax[1]), 0.5f * (rmin[2] + rmax[2]),
-                                     4.0f * (rmax[0] - rmin[0] + rmax[1] - rmin[1] + rmax[2] - rmin[2]));
-            } else {
-                pad[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-            }
+        float4 p1 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (mode == 1) {
+            p1 = make_float4(NAN, NAN, NAN, NAN);
+        } else if (mode == 2) {
+            const float c = 0.5f * (rmin[0] + rmax[0]);
+            p1 = make_float4(c, 0.5f * (rmin[1] + rmax[1]), 0.5f * (rmin[2] + rmax[2]),
+                             4.0f * (rmax[0] - rmin[0] + rmax[1] - rmin[1] + rmax[2] - rmin[2]));
         }
-        float4* tail = const_cast<float4*>(sc.prim_sp) + in.n_prim_refs;
+        float4 pad[kPrimPad];
+        for (uint32_t i = 0; i < kPrimPad; ++i) pad[i] = p1;
+        // the line-packed layout's gaps hold the same (RT_LEAF_PACK=1, an A/B
+        // switch read here; off by default: measured no faster)
+        r->prim_slots = in.n_prim_refs;
+        r->leaf_packed = false;
+        if (!sc.root_is_leaf && env_flag("RT_LEAF_PACK", RT_LEAF_PACK_DEFAULT) &&
+            (st = pack_leaf_lines(r, sc, in, p1)))
+            return st;
+        float4* tail = const_cast<float4*>(sc.prim_sp) + r->prim_slots;
         RT_HIP(r, hipMemcpyAsync(tail, pad, sizeof(pad), hipMemcpyHostToDevice, r->stream));
         RT_HIP(r, hipStreamSynchronize(r->stream));
     }
@@ -646,7 +740,7 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
         // the camera-relative screen records of this frame's camera origin
         // (DESIGN.md 5.1): remade on this stream, after the renderer's earlier
         // frames (order_after_last), when the origin or the scene changed
-        const uint32_t nr = r->info.n_prim_refs + kPrimPad;
+        const uint32_t nr = r->prim_slots + kPrimPad;
         const float4* before = r->d_prim_cam.p;
         if ((ost = ensure(r, r->d_prim_cam, nr))) return ost;
         if (r->d_prim_cam.p != before || r->cam_gen != r->scene_gen ||
@@ -1101,6 +1195,30 @@ int rt_export_octree(rt_renderer* r, uint32_t* nodes_out, float* prim_sp_out,
     if ((st = set_device(r))) return st;
     RT_HIP(r, hipDeviceSynchronize());
     const size_t nn = r->info.n_nodes, np = r->info.n_prim_refs;
+    if (r->leaf_packed) {
+        // the builders' record-for-record tree: the line-packed lists
+        // (pack_leaf_lines) put back to back again, in the same order
+        std::vector<uint2> nodes(nn);
+        RT_HIP(r, hipMemcpy(nodes.data(), r->sc.nodes, nn * sizeof(uint2), hipMemcpyDeviceToHost));
+        std::vector<float4> sp(r->prim_slots);
+        std::vector<uint32_t> ix(r->prim_slots);
+        if (r->prim_slots) {
+            RT_HIP(r, hipMemcpy(sp.data(), r->sc.prim_sp, sp.size() * sizeof(float4), hipMemcpyDeviceToHost));
+            RT_HIP(r, hipMemcpy(ix.data(), r->sc.prim_idx, ix.size() * sizeof(uint32_t),
+                                hipMemcpyDeviceToHost));
+        }
+        uint32_t off = 0;
+        for (uint32_t i : leaf_records(nodes)) {
+            uint2& rec = nodes[i];
+            if (prim_sp_out)
+                memcpy(prim_sp_out + 4u * size_t(off), sp.data() + rec.x, rec.y * sizeof(float4));
+            if (prim_idx_out) memcpy(prim_idx_out + off, ix.data() + rec.x, rec.y * sizeof(uint32_t));
+            rec.x = off;
+            off += rec.y;
+        }
+        if (nodes_out) memcpy(nodes_out, nodes.data(), nn * sizeof(uint2));
+        return RT_OK;
+    }
     if (nodes_out)
         RT_HIP(r, hipMemcpy(nodes_out, r->sc.nodes, nn * sizeof(uint2), hipMemcpyDeviceToHost));
     if (prim_sp_out && np)

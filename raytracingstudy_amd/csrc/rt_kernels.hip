@@ -290,6 +290,10 @@ __device__ __forceinline__ uint32_t leaf_buf_base(const SceneArgs& S, bool sorte
     return head + wave * kLeafBuf;
 }
 
+#ifndef RT_CAP_VALU
+#define RT_CAP_VALU 0
+#endif
+
 // LDS leaf staging by gfx950's direct global -> LDS load (RT_GLDS, VERDICT r05
 // item 5): ONE global_load_lds_dwordx4 writes spheres 0 .. cnt - 1 of the leaf
 // at src into dst[0 .. cnt - 1] without a VGPR round trip or a ds_write.  Its
@@ -308,11 +312,13 @@ __device__ __forceinline__ void glds_leaf(const float4* src, float4* dst, uint32
     typedef __attribute__((address_space(3))) float4 LdsF4;
     const uint32_t lds = __builtin_amdgcn_readfirstlane(
         static_cast<uint32_t>(reinterpret_cast<uintptr_t>((LdsF4*)dst)));
-    const uint64_t base = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(
-                               static_cast<uint32_t>(reinterpret_cast<uint64_t>(src) >> 32)))
-                           << 32) |
-                          __builtin_amdgcn_readfirstlane(
-                              static_cast<uint32_t>(reinterpret_cast<uint64_t>(src)));
+    // (the builtin returns int: each half goes through uint32_t, or the low
+    // half would be sign-extended into the high one)
+    const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(reinterpret_cast<uint64_t>(src) >> 32)));
+    const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(reinterpret_cast<uint64_t>(src))));
+    const uint64_t base = (static_cast<uint64_t>(hi) << 32) | lo;
     const uint64_t mask = (1ull << cnt) - 1ull;
     uint64_t save;
     uint32_t keep, off;
@@ -611,7 +617,16 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         // bookkeeping is one loop-exit mask update per trip (the scalar pipe is
         // this kernel's busiest unit, profiles/r02/pmc_sq_screen.json).
         bool any_hit = false;
+#if RT_CAP_VALU
+        // the trip counter as a lane value (an opaque v_mov): the cap test is
+        // one VALU compare feeding the exit mask, not SALU add / compare /
+        // select on the scalar pipe (A/B)
+        uint32_t it;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(it));
+        for (const uint32_t cap = 8u * G + 64u;; ++it) {
+#else
         for (uint32_t it = 0, cap = 8u * G + 64u;; ++it) {
+#endif
             RT_BS(kBsIter);
             if (kAnyHit) RT_BS(kBsIterShadow);
             uint2 rec = make_uint2(0u, 0u);

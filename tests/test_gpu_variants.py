@@ -151,6 +151,45 @@ def test_lds_staging_on_and_off(gpu, oracle, case, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("case", [(20000, 64, 48, 64, 7, 12), (20000, 128, 96, 2, 12, 8),
+                                  (30000, 40, 30, 256, 12, 10), (3000, 64, 48, 16, 7, 2)],
+                         ids=lambda c: "n%d_%dx%d_s%d_d%d_cap%d" % c)
+@pytest.mark.parametrize("pad_fill", [0, 1, 2])
+def test_leaf_lines_packed_and_not(gpu, oracle, case, pad_fill, monkeypatch):
+    """The line-packed leaf layout (RT_LEAF_PACK, read when the scene is
+    built) moves leaf lists so that none straddles a cache line
+    it fits in, leaving gaps filled like the kPrimPad tail.  Packed and
+    back-to-back layouts give the oracle's image, radiance and counters, with
+    any gap filling, and rt_export_octree returns the builders' compact tree
+    either way (record for record the oracle's)."""
+    n, w, h, spp, depth, cap = case
+    sp, al = rt.generate_spheres(n, rt.SEED)
+    out = {}
+    for pack in ("0", "1"):
+        monkeypatch.setenv("RT_LEAF_PACK", pack)
+        with rt.KernelRenderer(w, h, mode="scene", spp=spp, radiance=True, pad_fill=pad_fill) as r:
+            r.resize(w, h)
+            r.setPosition(rt.camera.scene_pose())
+            r.set_scene(sp, al, max_depth=depth, leaf_capacity=cap)
+            r.render()
+            img0 = r.readback()
+            st = r.render(stats=True)
+            img, rad = r.readback(), r.readback_radiance()
+            tree = r.export_octree()
+            _, K = r.camera()
+        out[pack] = (img0, img, rad, st, tree)
+    sc = oracle.Scene(sp, al, max_depth=depth, leaf_capacity=cap)
+    ref = sc.render(w, h, rt.camera.scene_pose(), K, spp=spp)
+    onodes, oidx = sc.export_bfs()
+    for pack, (img0, img, rad, st, (nodes, psp, pidx)) in out.items():
+        rep = vc.diff_report(img, rad, st, ref)
+        assert not rep, (pack, rep)
+        assert np.array_equal(img0, img), pack
+        assert np.array_equal(nodes, onodes) and np.array_equal(pidx, oidx), pack
+        assert np.array_equal(psp, sp[oidx]), pack
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,w,h,spp,jitter,tiles", [
     (30000, 70, 45, 256, None, False),   # four rounds (C5's shape), edge pixels
     (30000, 70, 45, 192, None, True),    # three rounds, packed tiles with off-image pixels
