@@ -135,6 +135,17 @@ struct rt_renderer {
     uint32_t frames_accum = 0;       // frames in `accum` (0: next frame starts over)
     uint64_t accum_sig = 0;          // which pixels the sums belong to (frame / tile list)
     DevBuf<unsigned long long> counters;
+    // the counters, queue heads and slot table in two sets of ctr_stride
+    // words: a scene frame uses set ctr_set and its kernel zeroes the other
+    // one for the next frame (FrameArgs::ctr_next), so no memset launch sits
+    // between frames; ctr_zero[s] = leading words of set s known to be zero
+    size_t ctr_stride = 0;
+    uint32_t ctr_set = 0;
+    size_t ctr_zero[2] = {0, 0};
+    // superblock claim order of full frames (FrameArgs::sb_order) and the
+    // superblock grid it was made for
+    DevBuf<uint32_t> sb_order;
+    uint32_t sb_nx = 0, sb_ny = 0;
     // device copies of recently used tile lists (rt_render_tiles: this rank's
     // list; rt_unpack_tiles on rank 0: one list per peer), least recently used
     // evicted; each host vector stays alive as the source of its async upload
@@ -346,6 +357,41 @@ const char* test_env(uint32_t flags, const char* name) {
     }
     return on ? v : nullptr;
 }
+
+// Superblock claim order (FrameArgs::sb_order, RT_SB_ORDER): the cells of a
+// Hilbert curve over the next power-of-two square, those inside the nx x ny
+// superblock grid in curve order, as row-major indices.  The level-1 counter
+// hands claims to the XCDs in turn, so an XCD's successive superblocks lie a
+// few steps apart along the curve, near each other in the image, instead of
+// eight columns apart in row-major order.
+std::vector<uint32_t> hilbert_order(uint32_t nx, uint32_t ny) {
+    uint32_t n = 1;
+    while (n < nx || n < ny) n *= 2u;
+    std::vector<uint32_t> out;
+    out.reserve(size_t(nx) * ny);
+    for (uint64_t d = 0; d < uint64_t(n) * n; ++d) {
+        uint32_t x = 0, y = 0;
+        uint64_t t = d;
+        for (uint32_t s = 1; s < n; s *= 2u) {
+            const uint32_t rx = 1u & static_cast<uint32_t>(t / 2), ry = 1u & static_cast<uint32_t>(t ^ rx);
+            if (ry == 0) {
+                if (rx == 1) {
+                    x = s - 1u - x;
+                    y = s - 1u - y;
+                }
+                std::swap(x, y);
+            }
+            x += s * rx;
+            y += s * ry;
+            t /= 4;
+        }
+        if (x < nx && y < ny) out.push_back(y * nx + x);
+    }
+    return out;
+}
+#ifndef RT_SB_ORDER_DEFAULT
+#define RT_SB_ORDER_DEFAULT 0
+#endif
 
 // Leaf records of a breadth-first tree: a record's kind is in
 // its parent's leaf mask, and children come after their parent, so one
@@ -722,7 +768,7 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     int ost;
     if ((ost = order_after_last(r, st))) return ost;
     // the counters and, for the wave queue, its per-XCD slot table (8 x
-    // (superblocks + 2) words after them): one buffer, one memset per frame
+    // (superblocks + 2) words after them): one set of `words`
     size_t words = kCounterWords;
     a.wq_slots = nullptr;
     a.wq_slot_stride = 0;
@@ -734,8 +780,35 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
         a.wq_slot_stride = (a.wq_slot_shift == 12u ? nsb : nbk) + 2u;
         words += (8u * static_cast<size_t>(a.wq_slot_stride) + 1u) / 2u;
     }
-    if ((ost = ensure(r, r->counters, words))) return ost;
-    if (a.wq_slot_stride) a.wq_slots = reinterpret_cast<uint32_t*>(r->counters.p + kCounterWords);
+    if (r->ctr_stride < words) {  // (re)allocate both sets and zero them
+        if ((ost = ensure(r, r->counters, 2 * words))) return ost;
+        r->ctr_stride = r->counters.n / 2;
+        RT_HIP(r, hipMemsetAsync(r->counters.p, 0, r->counters.n * sizeof(unsigned long long), st));
+        r->ctr_zero[0] = r->ctr_zero[1] = r->ctr_stride;
+    }
+    const uint32_t cs = r->ctr_set;
+    unsigned long long* ctr = r->counters.p + cs * r->ctr_stride;
+    if (r->ctr_zero[cs] < words)  // (after a failed launch, or a frame needing more words)
+        RT_HIP(r, hipMemsetAsync(ctr, 0, words * sizeof(unsigned long long), st));
+    if (a.wq_slot_stride) a.wq_slots = reinterpret_cast<uint32_t*>(ctr + kCounterWords);
+    a.sb_order = nullptr;
+    if (r->cfg.mode == RT_MODE_SCENE && !a.tiles && a.wq_slot_shift == 12u &&
+        env_flag("RT_SB_ORDER", RT_SB_ORDER_DEFAULT)) {
+        // the superblock grid of this frame (scene_body's nsx x nsy)
+        uint32_t spw, g, ppw, tw, th;
+        wave_tile_shape(a.spp, spw, g, ppw, tw, th);
+        const uint32_t gw = (a.W + tw - 1u) / tw, gh = (a.H + th - 1u) / th;
+        const uint32_t nx = ((gw + 7u) / 8u + 7u) / 8u, ny = ((gh + 7u) / 8u + 7u) / 8u;
+        if (r->sb_nx != nx || r->sb_ny != ny || !r->sb_order.p) {
+            const std::vector<uint32_t> ord = hilbert_order(nx, ny);
+            if ((ost = ensure(r, r->sb_order, ord.size()))) return ost;
+            RT_HIP(r, hipMemcpy(r->sb_order.p, ord.data(), ord.size() * sizeof(uint32_t),
+                                hipMemcpyHostToDevice));
+            r->sb_nx = nx;
+            r->sb_ny = ny;
+        }
+        a.sb_order = r->sb_order.p;
+    }
     if (r->cfg.mode == RT_MODE_SCENE) {
         // the camera-relative screen records of this frame's camera origin
         // (DESIGN.md 5.1): remade on this stream, after the renderer's earlier
@@ -797,8 +870,10 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
         }
         a.sc.prim_shd = r->d_prim_shd.p;
     }
-    a.counters = r->counters.p;
-    RT_HIP(r, hipMemsetAsync(r->counters.p, 0, words * sizeof(unsigned long long), st));
+    a.counters = ctr;
+    const bool scene = r->cfg.mode == RT_MODE_SCENE;
+    a.ctr_next = scene ? r->counters.p + (1u - cs) * r->ctr_stride : nullptr;
+    a.ctr_next_words = scene ? static_cast<uint32_t>(words) : 0u;
     if ((ost = poison_outputs(r, a, st))) return ost;
     a.count_work = stats ? 1u : 0u;
     a.test_fault_queue = r->test_fault_queue && !stats ? 1u : 0u;
@@ -829,7 +904,15 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     }
 #endif
     hipError_t e = r->cfg.mode == RT_MODE_SCENE ? launch_scene(a, st) : launch_compat(a, st);
-    if (e != hipSuccess) return hip_fail(r, e, "kernel launch");
+    if (e != hipSuccess) {
+        r->ctr_zero[0] = r->ctr_zero[1] = 0;  // neither set is known to be zero
+        return hip_fail(r, e, "kernel launch");
+    }
+    if (scene) {  // this frame dirtied its set and zeroes the other one
+        r->ctr_zero[cs] = 0;
+        r->ctr_zero[1u - cs] = words;
+        r->ctr_set = 1u - cs;
+    }
 #ifdef RT_BLOCK_STATS
     if (bs_file) {
         unsigned long long h[2 * kBlockStats];
@@ -861,7 +944,7 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
         RT_HIP(r, hipEventRecord(r->ev1, st));
         RT_HIP(r, hipEventSynchronize(r->ev1));
         unsigned long long lines[8 * kStatLineStride], c[4] = {0, 0, 0, 0};
-        RT_HIP(r, hipMemcpy(lines, r->counters.p + kStatLineBase, sizeof(lines), hipMemcpyDeviceToHost));
+        RT_HIP(r, hipMemcpy(lines, ctr + kStatLineBase, sizeof(lines), hipMemcpyDeviceToHost));
         for (uint32_t q = 0; q < 8; ++q)
             for (uint32_t i = 0; i < 4; ++i) c[i] += lines[q * kStatLineStride + i];
         float ms = 0.f;
@@ -1025,6 +1108,7 @@ int rt_destroy(rt_renderer* r) {
     r->d_albedo.release();
     r->d_prim_cam.release();
     r->d_prim_shd.release();
+    r->sb_order.release();
     r->gpu_build.release();
     r->cell_table.release();
     if (r->ev0) (void)hipEventDestroy(r->ev0);

@@ -264,6 +264,15 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
 #define RT_LDS_MIN 6
 #endif
 constexpr uint32_t kLdsLeafMin = RT_LDS_MIN;
+// Only nearest-hit (primary) walks stage their leaves: a shadow ray may stop
+// at a leaf's first chunk, after a staging load fetched all of the leaf's
+// lines, and its chunked reads stop with it.  Against staging shadow leaves
+// too (RT_LDS_SHADOW=1, A/B): C5d -1.3%, C5 -0.5%, C3 -0.1%
+// (profiles/r06/ab_ctr3_noshst_sbo.log, 3 alternating rounds).
+#ifndef RT_LDS_SHADOW
+#define RT_LDS_SHADOW 0
+#endif
+constexpr bool kLdsShadow = RT_LDS_SHADOW != 0;
 constexpr size_t kLeafBufBytes = RT_LDS_LEAF ? (kBlockThreads / 64u) * kLeafBuf * sizeof(float4) : 0u;
 
 // Ancestor-stack levels per thread: depths 1..D-1, or K..D-1 with a cell table
@@ -297,46 +306,28 @@ __device__ __forceinline__ uint32_t leaf_buf_base(const SceneArgs& S, bool sorte
 // LDS leaf staging by gfx950's direct global -> LDS load (RT_GLDS, VERDICT r05
 // item 5): ONE global_load_lds_dwordx4 writes spheres 0 .. cnt - 1 of the leaf
 // at src into dst[0 .. cnt - 1] without a VGPR round trip or a ds_write.  Its
-// LDS destination is M0 + 16 x lane id, so lane k must fetch sphere k: the
-// instruction runs with exec = lanes 0 .. cnt - 1 (cnt <= kLeafBuf = 32),
-// whichever of them are active in the walk (an inactive lane's sphere is
-// still in the leaf, its fetch in bounds), and the address is computed under
-// that exec too.  M0 and exec are restored in the same statement.  The load
-// is invisible to the compiler's waitcnt bookkeeping: the explicit vmcnt(0)
-// retires it before the chunks' ds_reads (the issuing wave is the reader, so
-// no barrier is needed; MI355X_MICROARCH.md item 7).
+// LDS destination is M0 + 16 x lane id, so it needs cnt consecutive active
+// lanes: from the wave's first active lane l0, lane l0 + k fetches sphere k
+// into (dst - l0)[l0 + k].  Returns false (the caller stages through
+// registers) when lanes l0 .. l0 + cnt - 1 are not all active.  (Widening
+// exec to lanes 0 .. cnt - 1 inside an asm statement instead, the first
+// build, was wrong: the address temporary's VGPR then changes in lanes the
+// compiler keeps other lanes' loop-exit values in; plain frames differed.)
+// The explicit vmcnt(0) retires the DMA before the chunks' ds_reads (the
+// issuing wave is the reader: no barrier, MI355X_MICROARCH.md item 7).
 #ifndef RT_GLDS
 #define RT_GLDS 0
 #endif
-__device__ __forceinline__ void glds_leaf(const float4* src, float4* dst, uint32_t cnt) {
-    typedef __attribute__((address_space(3))) float4 LdsF4;
-    const uint32_t lds = __builtin_amdgcn_readfirstlane(
-        static_cast<uint32_t>(reinterpret_cast<uintptr_t>((LdsF4*)dst)));
-    // (the builtin returns int: each half goes through uint32_t, or the low
-    // half would be sign-extended into the high one)
-    const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
-        static_cast<uint32_t>(reinterpret_cast<uint64_t>(src) >> 32)));
-    const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
-        static_cast<uint32_t>(reinterpret_cast<uint64_t>(src))));
-    const uint64_t base = (static_cast<uint64_t>(hi) << 32) | lo;
-    const uint64_t mask = (1ull << cnt) - 1ull;
-    uint64_t save;
-    uint32_t keep, off;
-    asm volatile(
-        "s_mov_b64 %[save], exec\n\t"
-        "s_mov_b64 exec, %[mask]\n\t"
-        "v_mbcnt_lo_u32_b32 %[off], -1, 0\n\t"
-        "v_lshlrev_b32 %[off], 4, %[off]\n\t"
-        "s_mov_b32 %[keep], m0\n\t"
-        "s_mov_b32 m0, %[lds]\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %[off], %[base]\n\t"
-        "s_mov_b32 m0, %[keep]\n\t"
-        "s_mov_b64 exec, %[save]\n\t"
-        "s_waitcnt vmcnt(0)"
-        : [save] "=&s"(save), [keep] "=&s"(keep), [off] "=&v"(off)
-        : [mask] "s"(mask), [lds] "s"(lds), [base] "s"(base)
-        : "memory");
+__device__ __forceinline__ bool glds_leaf(const float4* src, float4* dst, uint32_t cnt) {
+    typedef __attribute__((address_space(3))) void LdsV;
+    const uint64_t act = __ballot(1);
+    const uint32_t l0 = static_cast<uint32_t>(__builtin_ctzll(act));
+    const uint64_t run = ((1ull << cnt) - 1ull) << l0;  // cnt < kLeafBuf = 32
+    if (l0 + cnt > 64u || (act & run) != run) return false;
+    const uint32_t k = __lane_id() - l0;
+    if (k < cnt) __builtin_amdgcn_global_load_lds(src + k, (LdsV*)(dst - l0), 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return true;
 }
 
 // Grid-space octree walk (DESIGN.md "Octree walk"): mirrored origin so every
@@ -570,18 +561,17 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         // the exact tests skip as before.
         const uint32_t off_u = __builtin_amdgcn_readfirstlane(off);
         const uint32_t cnt_u = __builtin_amdgcn_readfirstlane(cnt);
-        if (cnt_u >= kLdsLeafMin && cnt_u < kernargs()->sc.lds_max && __all(off == off_u)) {
+        if ((kLdsShadow || !kAnyHit) && cnt_u >= kLdsLeafMin && cnt_u < kernargs()->sc.lds_max &&
+            __all(off == off_u)) {
             RT_BS(kBsLdsLeaf);
             extern __shared__ __attribute__((aligned(16))) float4 lds_leaf[];
             const uint32_t lb = leaf_buf_base(S, kNoStack);
             const float4* __restrict__ pu = prim_sp + off_u;
-#if RT_GLDS
-            glds_leaf(pu, lds_leaf + lb, cnt_u);
-#else
-            const uint64_t act = __ballot(1);
-            const uint32_t na = static_cast<uint32_t>(__popcll(act));
-            for (uint32_t k = lane_rank(act); k < cnt_u; k += na) lds_leaf[lb + k] = pu[k];
-#endif
+            if (!RT_GLDS || !glds_leaf(pu, lds_leaf + lb, cnt_u)) {
+                const uint64_t act = __ballot(1);
+                const uint32_t na = static_cast<uint32_t>(__popcll(act));
+                for (uint32_t k = lane_rank(act); k < cnt_u; k += na) lds_leaf[lb + k] = pu[k];
+            }
             // (a wave's LDS operations complete in order: the reads below see
             // the writes, and the compiler keeps them in order: same array)
             return chunks([&](uint32_t k) { return lds_leaf[lb + k]; }, off_u, cnt_u);
@@ -1290,6 +1280,15 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
                                                  stack_levels(a.sc, true) * kBlockThreads) +
                             wave * (kSortWaveBytes / 4u)
                       : nullptr;
+    // the next frame's counters, queue heads and slot table (the other set,
+    // FrameArgs::ctr_next): zeroed here by the first workgroup, so frames run
+    // back to back with no memset launch between them.  The previous frame,
+    // which used that set, completed before this one started.
+    // (fields read through kernargs(): nothing of this stays live in SGPRs)
+    if (blockIdx.x == 0) {
+        KernArgs* kz = kernargs();
+        for (uint32_t i = threadIdx.x; i < kz->ctr_next_words; i += kBlockThreads) kz->ctr_next[i] = 0ull;
+    }
     const uint32_t tw = a.tw, th = a.th;
     uint32_t n_shadow = 0, n_nodes = 0, n_prims = 0, n_primary = 0;
 #ifdef RT_BLOCK_STATS
@@ -1414,7 +1413,14 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
                 const uint32_t g = e - 1u;
                 if (ks == 12u) {
                     k = kTiles ? g / sb_grid : 0u;
-                    const uint32_t sg = g - k * sb_grid;
+                    uint32_t sg = g - k * sb_grid;
+                    // claim order -> superblock: row-major, or a space-filling
+                    // order (FrameArgs::sb_order, RT_SB_ORDER) in which an
+                    // XCD's successive claims lie near each other
+                    if (!kTiles) {
+                        const uint32_t* so = kernargs()->sb_order;
+                        if (so) sg = so[sg];
+                    }
                     sx0 = (sg % nsx) * 64u;
                     sy0 = (sg / nsx) * 64u;
                 } else {

@@ -244,7 +244,11 @@ struct FrameArgs {
     uint32_t n_tiles;
     uint32_t tile_size;
     uint32_t tiles_x;   // ceil(W / tile_size)
-    unsigned long long* counters;  // [primary, shadow, nodes, prims]
+    unsigned long long* counters;  // this frame's set: stat lines, queue heads, slot table
+    // the other set, which this frame's kernel zeroes (ctr_next_words words)
+    // for the next frame: frames need no memset launch between them
+    unsigned long long* ctr_next;
+    uint32_t ctr_next_words;
     uint32_t variant;   // scene kernel variant (kVariant*)
     // wave mapping (set by launch_scene): a wave = ppw pixels (tw x th) x spw samples
     uint32_t spw, g, ppw, tw, th, rounds;  // g = pow2ceil(spw) lanes per pixel
@@ -254,6 +258,8 @@ struct FrameArgs {
     uint32_t* wq_slots;        // two-level wave queue: per XCD, the superblock of each slot + 1
     uint32_t wq_slot_stride;   //   (0 = not claimed yet, kSlotNone = none left); zeroed per frame
     uint32_t wq_slot_shift;    //   slot = 2^shift wave tiles: 12 a superblock, 6 one 8x8 block
+    const uint32_t* sb_order;  // frame superblock slots: claim index -> superblock (a
+                               //   Hilbert order over the superblock grid), or null: row-major
     uint32_t wq_claim_delay;   // test only (RT_TEST_CLAIM_DELAY): XCD 0's ticket-0 wave sleeps
                                //   this many s_sleep 127 before claiming slot 0; 0 in product
     // Wave-queue failure report: a wave whose slot was never published (the

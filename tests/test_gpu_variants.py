@@ -190,6 +190,38 @@ def test_leaf_lines_packed_and_not(gpu, oracle, case, pad_fill, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("spp", [64, 256])
+def test_superblock_claim_order(gpu, oracle, spp, monkeypatch):
+    """The superblock claim order (RT_SB_ORDER, read per frame: row-major or
+    a Hilbert curve over the superblock grid) moves which XCD renders which
+    64x64 region, never a pixel: 1024x768 is 192 superblocks, the smallest
+    frame the queue claims in superblock slots; plain and stats frames give
+    the same image and counters either way, and every 64th row is the
+    oracle's."""
+    n, w, h = 3000, 1024, 768
+    sp, al = rt.generate_spheres(n, rt.SEED)
+    out = {}
+    for order in ("0", "1"):
+        monkeypatch.setenv("RT_SB_ORDER", order)
+        with rt.KernelRenderer(w, h, mode="scene", spp=spp, radiance=True) as r:
+            r.resize(w, h)
+            r.setPosition(rt.camera.scene_pose())
+            r.set_scene(sp, al)
+            r.render()
+            img0 = r.readback()
+            st = r.render(stats=True)
+            img, rad = r.readback(), r.readback_radiance()
+            _, K = r.camera()
+        assert np.array_equal(img0, img), order
+        out[order] = (img, rad, (st.primary_rays, st.shadow_rays, st.nodes_visited, st.prims_tested))
+    assert np.array_equal(out["0"][0], out["1"][0]) and np.array_equal(out["0"][1], out["1"][1])
+    assert out["0"][2] == out["1"][2]
+    ref8, ref32, _ = oracle.Scene(sp, al).render(w, h, rt.camera.scene_pose(), K, spp=spp, row_step=64)
+    rows = np.arange(0, h, 64)
+    assert np.array_equal(out["1"][0][rows], ref8[rows]) and np.array_equal(out["1"][1][rows], ref32[rows])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,w,h,spp,jitter,tiles", [
     (30000, 70, 45, 256, None, False),   # four rounds (C5's shape), edge pixels
     (30000, 70, 45, 192, None, True),    # three rounds, packed tiles with off-image pixels

@@ -5,6 +5,7 @@
 #   ab:<cfgs>:<reps>:<libs,...>   tools/ab_libs.sh over abl/librt_<lib>.so
 #   parity:<lib>   a parity subset with RT_AMD_LIB=abl/librt_<lib>.so
 #   pmcpack:<cfg>  counter passes with the leaf lists packed and not (RT_LEAF_PACK)
+#   pmcsq:<lib>:<cfg>  issue counters (SALU, VALU, branch, vector reads) of a library
 set -o pipefail
 OUT=${1:?out}; shift
 mkdir -p "$OUT"
@@ -39,6 +40,13 @@ for step in "$@"; do
             GRBM_GUI_ACTIVE || exit 1
       done
       python3 tools/pmc_probe_sum.py "$OUT"/pk_${cfg}_p* > "$OUT/pmc_pack_$cfg.json" || exit 1 ;;
+    pmcsq:*)
+      # issue counters of the timed kernel for a library (abl/librt_<lib>.so) and config
+      IFS=: read -r _ lib cfg <<< "$step"
+      RT_AMD_LIB=$PWD/abl/librt_$lib.so bash tools/pmc_probe.sh "${OUT#gpurun_out/}/sq_${lib}_$cfg" "$cfg" 0 \
+          SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAVES \
+          GRBM_GUI_ACTIVE || exit 1
+      python3 tools/pmc_probe_sum.py "$OUT/sq_${lib}_$cfg" > "$OUT/pmc_sq_${lib}_$cfg.json" || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
