@@ -259,9 +259,13 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
 // to the first chunk, which a leaf of one or two chunks does not win back.
 // Measured (profiles/r05/ldsmin_ab.log, 3 alternating rounds, against no
 // staging): from 1 / 4 / 6 / 8 spheres C3 +1.0 / -0.7 / -1.7 / +0.2%, C5
-// -6.9 / -7.8 / -7.8 / -5.3%, C5d +4.0 / +2.5 / +2.3 / +2.5%.
+// -6.9 / -7.8 / -7.8 / -5.3%, C5d +4.0 / +2.5 / +2.3 / +2.5%.  Round 6, with
+// shadow walks no longer staging (kLdsShadow), against 6: from 2 / 3 / 4 / 5
+// spheres C3 +0.2 / -0.4 / -0.5 / -1.0%, C5 -0.8 / -1.1 / -1.2 / -1.3%, C5d
+// +1.0 / +0.5 / +0.3 / +0.1%, 8: C3 +3.5%, C5 +4.6%
+// (profiles/r06/ab_r6_lmin2_lmin3_lmin4_lmin5.log, ab_r6_lmin4_lmin8.log).
 #ifndef RT_LDS_MIN
-#define RT_LDS_MIN 6
+#define RT_LDS_MIN 5
 #endif
 constexpr uint32_t kLdsLeafMin = RT_LDS_MIN;
 // Only nearest-hit (primary) walks stage their leaves: a shadow ray may stop
