@@ -27,6 +27,9 @@ lo = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 hi = int(sys.argv[2]) if len(sys.argv) > 2 else 1064
 budget = float(sys.argv[3]) if len(sys.argv) > 3 else 400.0
 oracle.load()
+# every frame sentinel-filled by the library too (RT_FLAG_TEST_POISON), stats
+# frames included, as in the test suite (tests/conftest.py)
+rt._lib.test_flags = rt._lib.RT_FLAG_TEST_POISON
 hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
 bad, t0 = [], time.time()
 done = 0
