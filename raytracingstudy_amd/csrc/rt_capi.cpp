@@ -36,6 +36,8 @@ hipError_t launch_cam_screen(const float4* prim_sp, uint32_t n, const float o[3]
                              hipStream_t st);
 hipError_t launch_shd_screen(const float4* prim_sp, uint32_t n, const float e[6], double delta,
                              float4* out, hipStream_t st);
+hipError_t launch_albedo_refs(const uint32_t* prim_idx, const uint32_t* albedo, uint32_t n,
+                              uint32_t n_spheres, uint32_t* out, hipStream_t st);
 }  // namespace rtamd
 
 using namespace rtamd;
@@ -193,6 +195,9 @@ struct rt_renderer {
     uint64_t shd_gen = ~0ull;
     float shd_e[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float cam_o[3] = {0.f, 0.f, 0.f};
+    // albedo by leaf reference (SceneArgs::prim_al) and the scene it was made for
+    DevBuf<uint32_t> d_prim_al;
+    uint64_t al_gen = ~0ull;
     rt_scene_info info{};
     std::string err;
     // multi-device handle (rt_create_multi): this renderer is devices[0]'s
@@ -869,6 +874,16 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
             r->shd_gen = r->scene_gen;
         }
         a.sc.prim_shd = r->d_prim_shd.p;
+        // the albedo of every leaf reference, made once per scene
+        const uint32_t* before_a = r->d_prim_al.p;
+        if ((ost = ensure(r, r->d_prim_al, nr))) return ost;
+        if (r->d_prim_al.p != before_a || r->al_gen != r->scene_gen) {
+            hipError_t e = launch_albedo_refs(a.sc.prim_idx, a.sc.albedo, r->prim_slots, r->n_spheres,
+                                              r->d_prim_al.p, st);
+            if (e != hipSuccess) return hip_fail(r, e, "albedo by leaf reference");
+            r->al_gen = r->scene_gen;
+        }
+        a.sc.prim_al = r->d_prim_al.p;
     }
     a.counters = ctr;
     const bool scene = r->cfg.mode == RT_MODE_SCENE;
@@ -1107,6 +1122,7 @@ int rt_destroy(rt_renderer* r) {
     r->d_spheres.release();
     r->d_albedo.release();
     r->d_prim_cam.release();
+    r->d_prim_al.release();
     r->d_prim_shd.release();
     r->sb_order.release();
     r->gpu_build.release();

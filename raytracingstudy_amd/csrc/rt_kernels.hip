@@ -277,6 +277,14 @@ constexpr uint32_t kLdsLeafMin = RT_LDS_MIN;
 #define RT_LDS_SHADOW 0
 #endif
 constexpr bool kLdsShadow = RT_LDS_SHADOW != 0;
+// Shading by leaf reference (SceneArgs::prim_al): a nearest walk's `iout` is
+// the hit's reference, and shading reads prim_sp[ref] / prim_al[ref]; 0 keeps
+// the sphere index (prim_idx[ref]) and the by-index spheres / albedo arrays.
+// Measured (profiles/r06/ab_ref_shade.log, 3 alternating rounds): C3 -0.7%,
+// C5 -0.5%, C5d -0.2%, C2 0; L2 misses C3 -7.5%, C5d -11.5% (pmc_l2_*.json)
+#ifndef RT_REF_SHADE
+#define RT_REF_SHADE 1
+#endif
 constexpr size_t kLeafBufBytes = RT_LDS_LEAF ? (kBlockThreads / 64u) * kLeafBuf * sizeof(float4) : 0u;
 
 // Ancestor-stack levels per thread: depths 1..D-1, or K..D-1 with a cell table
@@ -353,7 +361,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                                      float d1, float d2, float tmin, float tmax, float& tout,
                                      uint32_t& iout, uint32_t& n_nodes, uint32_t& n_prims,
                                      uint2* __restrict__ stk, bool any_rt = false,
-                                     uint32_t* bs = nullptr) {
+                                     uint32_t* bs = nullptr, uint32_t lb_u = ~0u) {
     static_assert(!kShadowL || kAnyHitT || kDynAny, "a shadow walk along L is an any-hit walk");
     const bool kAnyHit = kDynAny ? any_rt : kAnyHitT;
     const uint32_t D = S.max_depth;
@@ -569,7 +577,8 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             __all(off == off_u)) {
             RT_BS(kBsLdsLeaf);
             extern __shared__ __attribute__((aligned(16))) float4 lds_leaf[];
-            const uint32_t lb = leaf_buf_base(S, kNoStack);
+            // (lb_u: the caller's wave-uniform copy, an SGPR; else from threadIdx)
+            const uint32_t lb = lb_u != ~0u ? lb_u : leaf_buf_base(S, kNoStack);
             const float4* __restrict__ pu = prim_sp + off_u;
             if (!RT_GLDS || !glds_leaf(pu, lds_leaf + lb, cnt_u)) {
                 const uint64_t act = __ballot(1);
@@ -762,9 +771,9 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         if (any_hit) return true;
     }
     if (!kAnyHit && best_ref != kNoHit) {
-        RT_BS(kBsHitIdx);
+        if (!RT_REF_SHADE) RT_BS(kBsHitIdx);
         tout = best_t;
-        iout = S.prim_idx[best_ref];
+        iout = RT_REF_SHADE ? best_ref : S.prim_idx[best_ref];
         return true;
     }
     return false;
@@ -823,6 +832,18 @@ __device__ __forceinline__ void flush_counters(const FrameArgs& a, uint32_t prim
     }
 }
 
+// The hit record a nearest walk returned (`iout`: a leaf reference under
+// RT_REF_SHADE, else a sphere index): its sphere and its packed albedo.
+// (SA: SceneArgs, or the kernel arguments' copy behind kernargs())
+template <typename SA>
+__device__ __forceinline__ float4 hit_sphere_rec(SA& S, uint32_t h) {
+    return RT_REF_SHADE ? S.prim_sp[h] : S.spheres[h];
+}
+template <typename SA>
+__device__ __forceinline__ uint32_t hit_albedo(SA& S, uint32_t h) {
+    return RT_REF_SHADE ? S.prim_al[h] : S.albedo[h];
+}
+
 // Unified lane path: one walk instance run twice (primary, then the shadow ray
 // of the lanes that need one), so the register allocator sees one walk.
 template <int kChunk, bool kStats>
@@ -830,7 +851,8 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
                                                          uint32_t y, uint32_t hp, uint32_t s,
                                                          bool valid, uint32_t& n_shadow,
                                                          uint32_t& n_nodes, uint32_t& n_prims,
-                                                         void* stk, uint32_t* bs = nullptr) {
+                                                         void* stk, uint32_t* bs = nullptr,
+                                                         uint32_t lbs = ~0u) {
     const SceneArgs& S = a.sc;
     KernArgs* ka = kernargs();
     float u = static_cast<float>(x), v = static_cast<float>(y);
@@ -863,7 +885,7 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
             if (phase == 0)
                 hit = walk<false, kChunk, false, kStats>(S, r0, r1, r2, d0, d1, d2, 0.0f, INFINITY, t,
                                                          idx, n_nodes, n_prims,
-                                                         static_cast<uint2*>(stk), false, bs);
+                                                         static_cast<uint2*>(stk), false, bs, lbs);
             else {
                 // the shadow direction L is the frame's, the same in every
                 // lane: read afresh from the kernel arguments (SGPRs), not the
@@ -871,7 +893,7 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
                 KernArgs* kl = kernargs();
                 hit = walk<true, kChunk, false, kStats, false, true>(
                     S, r0, r1, r2, kl->L[0], kl->L[1], kl->L[2], 0.0f, INFINITY, t, idx, n_nodes,
-                    n_prims, static_cast<uint2*>(stk), true, bs);
+                    n_prims, static_cast<uint2*>(stk), true, bs, lbs);
             }
         }
         if (phase == 0) {
@@ -881,7 +903,7 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
             if (hit0) {
                 RT_BS(kBsShadeLoad);  // the sphere record
                 RT_BS(kBsShadeLoad);  // the albedo
-                const float4 sp = kb->sc.spheres[idx];
+                const float4 sp = hit_sphere_rec(kb->sc, idx);
                 const float p0 = r0 + t * d0;
                 const float p1 = r1 + t * d1;
                 const float p2 = r2 + t * d2;
@@ -892,7 +914,7 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
                 const float ndl = n0 * kb->L[0] + n1 * kb->L[1] + n2 * kb->L[2];
                 lam = ndl > 0.0f ? ndl : 0.0f;
                 want_shadow = ndl > 0.0f && kb->shadows;
-                al = kb->sc.albedo[idx];
+                al = hit_albedo(kb->sc, idx);
                 r0 = p0 + n0 * kShadowEps;
                 r1 = p1 + n1 * kShadowEps;
                 r2 = p2 + n2 * kShadowEps;
@@ -929,7 +951,8 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
                                                 uint32_t ox, uint32_t oy, uint32_t obase,
                                                 uint32_t& n_primary,
                                                 uint32_t& n_shadow, uint32_t& n_nodes,
-                                                uint32_t& n_prims, uint32_t* bs = nullptr) {
+                                                uint32_t& n_prims, uint32_t* bs = nullptr,
+                                                uint32_t lbs = ~0u) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t spw = a.spw, g = a.g;
     const uint32_t pix = lane / g, sub = lane & (g - 1u);
@@ -952,7 +975,7 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
         const bool valid = lane_ok && sg < s_end;
         n_primary += static_cast<uint32_t>(__popcll(__ballot(valid)));  // wave-uniform
         PixelOut c = sample_color_unified<kChunk, kStats>(a, x, y, hp, sg, valid, n_shadow,
-                                                          n_nodes, n_prims, stk, bs);
+                                                          n_nodes, n_prims, stk, bs, lbs);
         // Pixel sum of this round: pairwise butterfly over the pixel's g
         // lanes (missing samples are 0) = oracle.c:tree_sum; rounds are then
         // added in order in the leader's LDS slot.
@@ -1042,7 +1065,7 @@ struct HitShade {
 __device__ __forceinline__ HitShade hit_shade(float d0, float d1, float d2, float t, uint32_t idx,
                                               uint32_t* bs = nullptr) {
     KernArgs* kb = kernargs();
-    const float4 sp = kb->sc.spheres[idx];
+    const float4 sp = hit_sphere_rec(kb->sc, idx);
     RT_BS(kBsShadeLoad);
     HitShade h;
     h.p0 = kb->cam.o[0] + t * d0;
@@ -1070,7 +1093,7 @@ __device__ __forceinline__ void shade_pixel_sorted(const FrameArgs& a, float* wl
                                                    uint32_t x, uint32_t y, uint32_t obase,
                                                    uint32_t& n_primary, uint32_t& n_shadow,
                                                    uint32_t& n_nodes, uint32_t& n_prims,
-                                                   uint32_t* bs) {
+                                                   uint32_t* bs, uint32_t lbs) {
     const SceneArgs& S = a.sc;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t R = a.rounds;
@@ -1131,7 +1154,8 @@ __device__ __forceinline__ void shade_pixel_sorted(const FrameArgs& a, float* wl
             KernArgs* kc = kernargs();
             hit = walk<false, kChunk, true, kStats, true>(S, kc->cam.o[0], kc->cam.o[1], kc->cam.o[2],
                                                           d0, d1, d2, 0.0f, INFINITY, t, idx, n_nodes,
-                                                          n_prims, static_cast<uint2*>(stk), false, bs);
+                                                          n_prims, static_cast<uint2*>(stk), false, bs,
+                                                          lbs);
         }
         bool is_lit = false;
         if (valid) {
@@ -1146,7 +1170,7 @@ __device__ __forceinline__ void shade_pixel_sorted(const FrameArgs& a, float* wl
                 } else {
                     RT_BS(kBsShadeLoad);
                     sv = make_uint2(__float_as_uint(h.ndl > 0.0f ? h.ndl : 0.0f),
-                                    kernargs()->sc.albedo[idx]);
+                                    hit_albedo(kernargs()->sc, idx));
                     kd = 1;
                 }
             }
@@ -1185,11 +1209,11 @@ __device__ __forceinline__ void shade_pixel_sorted(const FrameArgs& a, float* wl
             uint32_t is;
             occ = walk<false, kChunk, true, kStats, true, true>(
                 S, o0, o1, o2, kl->L[0], kl->L[1], kl->L[2], 0.0f, INFINITY, ts, is, n_nodes,
-                n_prims, static_cast<uint2*>(stk), true, bs);
+                n_prims, static_cast<uint2*>(stk), true, bs, lbs);
         }
         if (has) {
             RT_BS(kBsShadeLoad);
-            slot[sl] = make_uint2(__float_as_uint(occ ? 0.0f : lam), kernargs()->sc.albedo[idx]);
+            slot[sl] = make_uint2(__float_as_uint(occ ? 0.0f : lam), hit_albedo(kernargs()->sc, idx));
             kind[sl] = 1;
         }
     }
@@ -1284,6 +1308,16 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
                                                  stack_levels(a.sc, true) * kBlockThreads) +
                             wave * (kSortWaveBytes / 4u)
                       : nullptr;
+    // the walks' LDS leaf buffer base as a wave-uniform value (an SGPR, or a
+    // lane of the SGPR spill VGPR), handed down to walk(): computed from
+    // threadIdx inside the walk it lived in a VGPR, which the sorted 64-VGPR
+    // build spilled to scratch and reloaded (a scratch load and a vmcnt(0)
+    // wait) on every staged leaf.  C5 -1.2%, C5d -0.3% (sorted), C3 -0.4%
+    // (profiles/r06/ab_leaf_base_*.log); RT_LB_SGPR=0: as before
+#ifndef RT_LB_SGPR
+#define RT_LB_SGPR 1
+#endif
+    const uint32_t lbs = RT_LB_SGPR ? __builtin_amdgcn_readfirstlane(leaf_buf_base(a.sc, kSort)) : ~0u;
     // the next frame's counters, queue heads and slot table (the other set,
     // FrameArgs::ctr_next): zeroed here by the first workgroup, so frames run
     // back to back with no memset launch between them.  The previous frame,
@@ -1462,10 +1496,10 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
 #endif
                 if (kSort)
                     shade_pixel_sorted<kTiles, kChunk, kStats, kProg>(
-                        a, wl, stk, ox, oy, obase, n_primary, n_shadow, n_nodes, n_prims, bs);
+                        a, wl, stk, ox, oy, obase, n_primary, n_shadow, n_nodes, n_prims, bs, lbs);
                 else
                     shade_wave_tile<kTiles, kChunk, kStats, kProg>(
-                        a, acc, stk, ox, oy, obase, n_primary, n_shadow, n_nodes, n_prims, bs);
+                        a, acc, stk, ox, oy, obase, n_primary, n_shadow, n_nodes, n_prims, bs, lbs);
 #ifdef RT_TIMELINE
                 // per unit {start, end, hw_id << 32 | xcc << 16 | wave index}
                 // after the 65536 per-wave records
@@ -1519,7 +1553,7 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
 #endif
                 shade_wave_tile<kTiles, kChunk, kStats, kProg>(
                     a, acc, stk, ox + wox, oy + woy, obase, n_primary, n_shadow, n_nodes,
-                    n_prims, bs);
+                    n_prims, bs, lbs);
 #ifdef RT_TIMELINE
                 // per wave tile of a block tile: {start, end, hw_id << 32 | xcc << 16 |
                 // wave index}, unit id = block tile * 16 + wave tile (tools/timeline.py)
@@ -1624,6 +1658,26 @@ hipError_t launch_cam_screen(const float4* prim_sp, uint32_t n, const float o[3]
     if (n) {
         hipLaunchKernelGGL(cam_screen_kernel, dim3((n + kBlockThreads - 1) / kBlockThreads),
                            dim3(kBlockThreads), 0, st, prim_sp, n, o[0], o[1], o[2], out);
+    }
+    return hipGetLastError();
+}
+
+// Albedo by leaf reference (SceneArgs::prim_al): out[i] = albedo[prim_idx[i]]
+// for the n real reference slots (a packed layout's gaps name sphere 0).
+__global__ void __launch_bounds__(kBlockThreads)
+    albedo_refs_kernel(const uint32_t* __restrict__ prim_idx, const uint32_t* __restrict__ albedo,
+                       uint32_t n, uint32_t n_spheres, uint32_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * kBlockThreads + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = prim_idx[i];
+    out[i] = k < n_spheres ? albedo[k] : 0u;
+}
+
+hipError_t launch_albedo_refs(const uint32_t* prim_idx, const uint32_t* albedo, uint32_t n,
+                              uint32_t n_spheres, uint32_t* out, hipStream_t st) {
+    if (n) {
+        hipLaunchKernelGGL(albedo_refs_kernel, dim3((n + kBlockThreads - 1) / kBlockThreads),
+                           dim3(kBlockThreads), 0, st, prim_idx, albedo, n, n_spheres, out);
     }
     return hipGetLastError();
 }

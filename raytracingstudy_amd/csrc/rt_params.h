@@ -197,6 +197,13 @@ struct SceneArgs {
     // made once per scene and light (shd_screen_kernel).  Shadow rays (any-hit,
     // direction L) screen a sphere by (u_p - u)^2 + (v_p - v)^2 <= rr'.
     const float4* prim_shd;
+    // Albedo by leaf reference (albedo[prim_idx[ref]], made once per scene,
+    // albedo_refs_kernel): a nearest walk returns its hit's REFERENCE, and the
+    // hit is shaded from prim_sp[ref] and prim_al[ref], lines the walk's own
+    // exact test and its neighbours just read, instead of three dependent
+    // loads of lines by sphere index (prim_idx, spheres, albedo) that miss the
+    // L2 (RT_REF_SHADE)
+    const uint32_t* prim_al;
     // LDS leaf staging: leaves of kLdsLeafMin .. lds_max - 1
     // spheres are staged; kLeafBuf, or 0 (off) under RT_LDS_STAGE=0 (A/B:
     // off at run time loses on every config, C5d included,

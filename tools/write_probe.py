@@ -26,13 +26,15 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--frames", type=int, default=4)
+    ap.add_argument("--no-shadows", action="store_true",
+                    help="primary rays only (RT_FLAG_NO_SHADOWS): tools/r6_gpu.sh pmcphase")
     args = ap.parse_args()
     import raytracingstudy_amd as rt
     from raytracingstudy_amd.camera import scene_pose
     c = rt.CONFIGS[args.config]
     sp, al = rt.configs.scene_spheres(c, rt.SEED)
     with rt.KernelRenderer(c.width, c.height, mode="scene", spp=c.spp,
-                           opt_off=(args.chunk & 7) << 4) as r:
+                           opt_off=(args.chunk & 7) << 4, shadows=not args.no_shadows) as r:
         r.resize(c.width, c.height)
         r.setPosition(scene_pose())
         r.set_scene(sp, al, max_depth=c.max_depth, leaf_capacity=c.leaf_capacity)
