@@ -35,7 +35,7 @@ hipError_t launch_unpack(const uint32_t* packed, const uint32_t* tiles, uint32_t
 hipError_t launch_cam_screen(const float4* prim_sp, uint32_t n, const float o[3], float4* out,
                              hipStream_t st);
 hipError_t launch_shd_screen(const float4* prim_sp, uint32_t n, const float e[6], double delta,
-                             float4* out, hipStream_t st);
+                             float4* out, float2* out8, uint32_t* rr_max, hipStream_t st);
 hipError_t launch_albedo_refs(const uint32_t* prim_idx, const uint32_t* albedo, uint32_t n,
                               uint32_t n_spheres, uint32_t* out, hipStream_t st);
 }  // namespace rtamd
@@ -195,6 +195,11 @@ struct rt_renderer {
     uint64_t shd_gen = ~0ull;
     float shd_e[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float cam_o[3] = {0.f, 0.f, 0.f};
+    // the light-plane records in 8 bytes (SceneArgs::prim_shd8) and their
+    // radius term (FrameArgs::shd_rr; rr_dev: the kernel's max, in bits)
+    DevBuf<float2> d_prim_shd8;
+    DevBuf<uint32_t> d_shd_rr;
+    float shd_rr = 0.0f;
     // albedo by leaf reference (SceneArgs::prim_al) and the scene it was made for
     DevBuf<uint32_t> d_prim_al;
     uint64_t al_gen = ~0ull;
@@ -852,8 +857,11 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
             a.shd_e[3 + i] = static_cast<float>(e2[i]);
         }
         const float4* before_s = r->d_prim_shd.p;
+        const float2* before_s8 = r->d_prim_shd8.p;
         if ((ost = ensure(r, r->d_prim_shd, nr))) return ost;
-        if (r->d_prim_shd.p != before_s || r->shd_gen != r->scene_gen ||
+        if ((ost = ensure(r, r->d_prim_shd8, nr))) return ost;
+        if ((ost = ensure(r, r->d_shd_rr, 1))) return ost;
+        if (r->d_prim_shd.p != before_s || r->d_prim_shd8.p != before_s8 || r->shd_gen != r->scene_gen ||
             memcmp(r->shd_e, a.shd_e, sizeof(r->shd_e)) != 0) {
             // M bounds |origin| and |centre| of every shadow test: the root
             // box holds every sphere, and a shadow origin is a hit point
@@ -868,12 +876,21 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
                 m = std::max(m, sqrt(q));
             }
             const double delta = kShadowSlackM / 16777216.0 * (m + 1e-4);
-            hipError_t e = launch_shd_screen(a.sc.prim_sp, nr, a.shd_e, delta, r->d_prim_shd.p, st);
+            RT_HIP(r, hipMemsetAsync(r->d_shd_rr.p, 0, sizeof(uint32_t), st));
+            hipError_t e = launch_shd_screen(a.sc.prim_sp, nr, a.shd_e, delta, r->d_prim_shd.p,
+                                             r->d_prim_shd8.p, r->d_shd_rr.p, st);
             if (e != hipSuccess) return hip_fail(r, e, "light-plane screen records");
+            // the 8-byte records' radius term, once per scene and light (a sync)
+            uint32_t bits = 0;
+            RT_HIP(r, hipMemcpyAsync(&bits, r->d_shd_rr.p, sizeof(bits), hipMemcpyDeviceToHost, st));
+            RT_HIP(r, hipStreamSynchronize(st));
+            memcpy(&r->shd_rr, &bits, sizeof(bits));
             memcpy(r->shd_e, a.shd_e, sizeof(r->shd_e));
             r->shd_gen = r->scene_gen;
         }
         a.sc.prim_shd = r->d_prim_shd.p;
+        a.sc.prim_shd8 = r->d_prim_shd8.p;
+        a.shd_rr = r->shd_rr;
         // the albedo of every leaf reference, made once per scene
         const uint32_t* before_a = r->d_prim_al.p;
         if ((ost = ensure(r, r->d_prim_al, nr))) return ost;
@@ -1123,6 +1140,8 @@ int rt_destroy(rt_renderer* r) {
     r->d_albedo.release();
     r->d_prim_cam.release();
     r->d_prim_al.release();
+    r->d_prim_shd8.release();
+    r->d_shd_rr.release();
     r->d_prim_shd.release();
     r->sb_order.release();
     r->gpu_build.release();

@@ -285,6 +285,20 @@ constexpr bool kLdsShadow = RT_LDS_SHADOW != 0;
 #ifndef RT_REF_SHADE
 #define RT_REF_SHADE 1
 #endif
+// Light-plane records in 8 bytes (SceneArgs::prim_shd8): a shadow chunk's two
+// spheres in ONE dwordx4 (the texture path charges a load by instruction,
+// not by bytes: 16 cycles for a dwordx2 or a dwordx4), screened against the
+// scene's largest radius term.  C3 -2.0%, C5 -2.4%, C2 -2.8%, C5d -0.1%; the
+// looser radius sends 2% (C3, C5) to 6% (C5d) more shadow chunks down the
+// exact path (profiles/r06/ab_shd8.log, bstats_shd8.log).  0: 16-byte records
+#ifndef RT_SHD8
+#define RT_SHD8 1
+#endif
+// spheres per chunk of the shadow walks (with 8-byte records: two per dwordx4);
+// 4 spills 48-100 B and runs C3 +6%, C5 +8%, C5d +5% (profiles/r06/ab_shd_chunk4.log)
+#ifndef RT_SHD_CHUNK
+#define RT_SHD_CHUNK 2
+#endif
 constexpr size_t kLeafBufBytes = RT_LDS_LEAF ? (kBlockThreads / 64u) * kLeafBuf * sizeof(float4) : 0u;
 
 // Ancestor-stack levels per thread: depths 1..D-1, or K..D-1 with a cell table
@@ -387,6 +401,9 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
 #endif
     const bool shd = kShdOk && kShadowL && kAnyHit;  // a shadow ray along L (the caller says so)
     float up = 0.0f, vp = 0.0f;
+    const bool shd8 = RT_SHD8 && kChunk % 2 == 0 && shd;
+    const float2* __restrict__ shd8_base = shd8 ? S.prim_shd8 : nullptr;
+    const float shd_rr = shd8 ? kernargs()->shd_rr : 0.0f;
     if (shd) {
         KernArgs* ke = kernargs();
         up = fmaf(o2, ke->shd_e[2], fmaf(o1, ke->shd_e[1], o0 * ke->shd_e[0]));
@@ -490,6 +507,17 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             // costs the texture path as much for one lane as for 64, and at
             // a leaf's odd end the whole wave usually has no slot 1
             bool fetched[kChunk];
+            if (shd8) {
+                // two slots' {u, v} per dwordx4 (8-byte aligned: global loads
+                // need dword alignment only; shd8 implies an even kChunk)
+#pragma unroll
+                for (int h = 0; h < kChunk / 2; ++h) {
+                    const float4 pr = *reinterpret_cast<const float4*>(shd8_base + (off + j + 2u * h));
+                    sv[2 * h] = make_float4(pr.x, pr.y, 0.0f, 0.0f);
+                    sv[2 * h + 1] = make_float4(pr.z, pr.w, 0.0f, 0.0f);
+                    fetched[2 * h] = fetched[2 * h + 1] = true;
+                }
+            } else
 #pragma unroll
             for (int q = 0; q < kChunk; ++q) {
 #ifdef RT_SKIP_PAST_END
@@ -529,7 +557,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                     // the centre's light-plane distance from the origin; rr'
                     // covers the rounding, so every sphere isect accepts passes
                     const float du = up - sv[q].x, dv = vp - sv[q].y;
-                    pos = !(fmaf(dv, dv, du * du) > sv[q].z);
+                    pos = !(fmaf(dv, dv, du * du) > (shd8 ? shd_rr : sv[q].z));
                 } else {
                     pos = !(isect_h(o0, o1, o2, d0, d1, d2, sv[q]) < 0.0f);
                 }
@@ -891,7 +919,7 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
                 // lane: read afresh from the kernel arguments (SGPRs), not the
                 // lanes' d registers
                 KernArgs* kl = kernargs();
-                hit = walk<true, kChunk, false, kStats, false, true>(
+                hit = walk<true, RT_SHD_CHUNK, false, kStats, false, true>(
                     S, r0, r1, r2, kl->L[0], kl->L[1], kl->L[2], 0.0f, INFINITY, t, idx, n_nodes,
                     n_prims, static_cast<uint2*>(stk), true, bs, lbs);
             }
@@ -1207,7 +1235,7 @@ __device__ __forceinline__ void shade_pixel_sorted(const FrameArgs& a, float* wl
             KernArgs* kl = kernargs();
             float ts;
             uint32_t is;
-            occ = walk<false, kChunk, true, kStats, true, true>(
+            occ = walk<false, RT_SHD_CHUNK, true, kStats, true, true>(
                 S, o0, o1, o2, kl->L[0], kl->L[1], kl->L[2], 0.0f, INFINITY, ts, is, n_nodes,
                 n_prims, static_cast<uint2*>(stk), true, bs, lbs);
         }
@@ -1631,7 +1659,8 @@ __global__ void __launch_bounds__(kBlockThreads)
 // this scene (kShadowSlackM u M).  One thread per reference.
 __global__ void __launch_bounds__(kBlockThreads)
     shd_screen_kernel(const float4* __restrict__ prim_sp, uint32_t n, float e0, float e1, float e2,
-                      float e3, float e4, float e5, double delta, float4* __restrict__ out) {
+                      float e3, float e4, float e5, double delta, float4* __restrict__ out,
+                      float2* __restrict__ out8, uint32_t* __restrict__ rr_max) {
     const uint32_t i = blockIdx.x * kBlockThreads + threadIdx.x;
     if (i >= n) return;
     const float4 c = prim_sp[i];
@@ -1639,16 +1668,22 @@ __global__ void __launch_bounds__(kBlockThreads)
     const double v = static_cast<double>(c.x) * e3 + static_cast<double>(c.y) * e4 + static_cast<double>(c.z) * e5;
     const double ur = 1.0 / 16777216.0;
     const double rg = static_cast<double>(c.w) * (1.0 + 4.0 * ur) + delta;
-    out[i] = make_float4(static_cast<float>(u), static_cast<float>(v),
-                         __double2float_ru(rg * rg * (1.0 + 4.0 * ur)), 0.0f);
+    const float rr = __double2float_ru(rg * rg * (1.0 + 4.0 * ur));
+    out[i] = make_float4(static_cast<float>(u), static_cast<float>(v), rr, 0.0f);
+    if (out8) {
+        out8[i] = make_float2(static_cast<float>(u), static_cast<float>(v));
+        // the largest rr' (non-negative floats order as their bits; a NaN
+        // radius, the test-only pad fill, orders above every number)
+        atomicMax(rr_max, __float_as_uint(rr));
+    }
 }
 
 hipError_t launch_shd_screen(const float4* prim_sp, uint32_t n, const float e[6], double delta,
-                             float4* out, hipStream_t st) {
+                             float4* out, float2* out8, uint32_t* rr_max, hipStream_t st) {
     if (n) {
         hipLaunchKernelGGL(shd_screen_kernel, dim3((n + kBlockThreads - 1) / kBlockThreads),
                            dim3(kBlockThreads), 0, st, prim_sp, n, e[0], e[1], e[2], e[3], e[4], e[5],
-                           delta, out);
+                           delta, out, out8, rr_max);
     }
     return hipGetLastError();
 }

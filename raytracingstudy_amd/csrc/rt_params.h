@@ -197,6 +197,10 @@ struct SceneArgs {
     // made once per scene and light (shd_screen_kernel).  Shadow rays (any-hit,
     // direction L) screen a sphere by (u_p - u)^2 + (v_p - v)^2 <= rr'.
     const float4* prim_shd;
+    // The same records in 8 bytes, {u, v} per reference (RT_SHD8): one
+    // dwordx4 carries a chunk's two; the radius term is the scene's largest
+    // rr' (FrameArgs::shd_rr), so the screen passes a superset still
+    const float2* prim_shd8;
     // Albedo by leaf reference (albedo[prim_idx[ref]], made once per scene,
     // albedo_refs_kernel): a nearest walk returns its hit's REFERENCE, and the
     // hit is shaded from prim_sp[ref] and prim_al[ref], lines the walk's own
@@ -237,6 +241,7 @@ struct FrameArgs {
     uint32_t contract;  // compat: 1 = getRay with nvcc-style FMA contraction (RT_FLAG_COMPAT_FMA)
     float L[3];         // unit vector toward the light
     float shd_e[6];     // light-plane basis {e1, e2} (orthonormal, perpendicular to L; f32)
+    float shd_rr;       // the largest light-plane rr' of the scene (SceneArgs::prim_shd8)
     float ambient;
     float inv_spp;      // 1 / samples in the image (all accumulated frames)
     // progressive accumulation (RT_FLAG_PROGRESSIVE)
