@@ -55,6 +55,7 @@ def load() -> ctypes.CDLL:
                                           ctypes.c_int]),
         "orc_max_threads": (ctypes.c_int, []),
         "orc_cam_screen_check": (None, [_P, _P, _P, _P, _u32, ctypes.c_double, ctypes.c_double, _P]),
+        "orc_cam8_screen_check": (None, [_P, _P, _u32, _P, _P, _P, _u32, ctypes.c_double, _P]),
         "orc_shd_screen_check": (None, [_P, _P, _P, _P, _u32, ctypes.c_double, ctypes.c_double,
                                         ctypes.c_double, _P]),
     }
@@ -211,6 +212,22 @@ def cam_screen_check(o, dirs, spheres, idx, slack_oc: float, slack_r: float):
     out = np.zeros(3, np.uint64)
     load().orc_cam_screen_check(_p(oa), _p(d), _p(sp), _p(ix), d.shape[0], float(slack_oc),
                                 float(slack_r), _p(out))
+    return int(out[0]), int(out[1]), int(out[2])
+
+
+def cam8_screen_check(o, B, ok: int, dirs, spheres, idx, shrink: float = 1.0):
+    """Test-only check of the product's 8-byte image-plane screen (oracle.c
+    orc_cam8_screen_check): (exact-accepted pairs the screen rejects, pairs
+    the screen passes, pairs the exact discriminant accepts)."""
+    oa = _f32(o, 3)
+    ba = _f32(B, 9)
+    d = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
+    sp = np.ascontiguousarray(spheres, np.float32).reshape(-1, 4)
+    ix = np.ascontiguousarray(idx, np.uint32).reshape(-1)
+    assert ix.shape[0] == d.shape[0]
+    out = np.zeros(3, np.uint64)
+    load().orc_cam8_screen_check(_p(oa), _p(ba), int(ok), _p(d), _p(sp), _p(ix), d.shape[0],
+                                 float(shrink), _p(out))
     return int(out[0]), int(out[1]), int(out[2])
 
 

@@ -509,6 +509,95 @@ void orc_cam_screen_check(const float o[3], const float* dirs, const float* sp, 
     }
 }
 
+/* Test-only: the product's image-plane screen of primary rays (rt_kernels.hip
+ * cam8_screen_kernel and walk<>'s cam8 chunk screen; rt_capi.cpp cam8_basis
+ * makes the basis B, rows x, y, z in f32) against the exact discriminant of
+ * isect, for m (direction, sphere) pairs from camera origin o.  The record
+ * is made as the kernel makes it (f64, rho^2 as bf16 in the low bytes of
+ * {qx, qy}); the lane's point from its f32 direction with each of the three
+ * f32 values next to 1/pz (the GPU's v_rcp_f32 is within 1 ulp), and a pair
+ * counts as passed only if all three pass.  shrink scales rho (1 = the
+ * product; < 1 must be seen to miss).  out[0] = pairs the exact test accepts
+ * and the screen rejects (must be 0), out[1] = pairs passed, out[2] = pairs
+ * the exact test accepts. */
+void orc_cam8_screen_check(const float o[3], const float B[9], uint32_t ok, const float* dirs,
+                           const float* sp, const uint32_t* idx, uint32_t m, double shrink,
+                           uint64_t out[3]) {
+    out[0] = out[1] = out[2] = 0;
+    for (uint32_t k = 0; k < m; ++k) {
+        const float* d = dirs + 3u * k;
+        const float* s = sp + 4u * idx[k];
+        /* the record (cam8_screen_kernel) */
+        const double vx = (double)s[0] - o[0], vy = (double)s[1] - o[1], vz = (double)s[2] - o[2];
+        const double X = (double)B[0] * vx + (double)B[1] * vy + (double)B[2] * vz;
+        const double Y = (double)B[3] * vx + (double)B[4] * vy + (double)B[5] * vz;
+        const double Z = (double)B[6] * vx + (double)B[7] * vy + (double)B[8] * vz;
+        const double dist = sqrt(vx * vx + vy * vy + vz * vz);
+        const double rp = (double)s[3] * (1.0 + 1e-6);
+        uint32_t hx = 0u, hy = 0u, rb = 0x7F800000u;
+        int pass_all = !ok || !(dist > rp * 1.0001) || !(Z > 0.0) || !isfinite(dist) || !(s[3] >= 0.0f);
+        if (!pass_all) {
+            const double az = Z / dist;
+            const double beta = acos(fmin(1.0, az));
+            const double th = asin(fmin(1.0, rp / dist));
+            if (!(beta + th < 1.45)) {
+                pass_all = 1;
+            } else {
+                const float qx = (float)(X / Z), qy = (float)(Y / Z);
+                const double q = fabs((double)qx) + fabs((double)qy);
+                const double rho_g = sin(th) / (az * cos(beta + th));
+                const double eps_c = 1.5 * (1.0 / 16384.0) * q;
+                const double mm = 1.0 + q + rho_g;
+                const double rho = (rho_g * (1.0 + 1e-5) + eps_c + 4e-6 * mm * mm) * shrink;
+                const double r2d = rho * rho * (1.0 + 1e-6);
+                float r2 = (float)r2d;
+                if ((double)r2 < r2d) r2 = nextafterf(r2, INFINITY); /* toward +inf */
+                uint32_t bits;
+                memcpy(&bits, &r2, 4);
+                if (bits & 0xFFFFu) bits = (bits & 0xFFFF0000u) + 0x10000u;
+                if (isfinite(r2) && bits < 0x7F800000u) {
+                    rb = bits;
+                    memcpy(&hx, &qx, 4);
+                    memcpy(&hy, &qy, 4);
+                } else {
+                    pass_all = 1;
+                }
+            }
+        }
+        const uint32_t sxb = (hx & ~0xFFu) | (rb >> 24), syb = (hy & ~0xFFu) | ((rb >> 16) & 0xFFu);
+        float rqx, rqy, rho2;
+        memcpy(&rqx, &sxb, 4);
+        memcpy(&rqy, &syb, 4);
+        const uint32_t rbits = ((sxb & 0xFFu) << 24) | ((syb & 0xFFu) << 16); /* v_perm_b32 0x04000C0C */
+        memcpy(&rho2, &rbits, 4);
+        /* the lane (walk<> cam8) */
+        const float px = fmaf(B[2], d[2], fmaf(B[1], d[1], B[0] * d[0]));
+        const float py = fmaf(B[5], d[2], fmaf(B[4], d[1], B[3] * d[0]));
+        const float pz = fmaf(B[8], d[2], fmaf(B[7], d[1], B[6] * d[0]));
+        const float iz0 = 1.0f / pz;
+        const float izs[3] = {nextafterf(iz0, -INFINITY), iz0, nextafterf(iz0, INFINITY)};
+        int pass = 1;
+        for (int v = 0; v < 3; ++v) {
+            const float s8x = px * izs[v], s8y = py * izs[v];
+            const float dx = s8x - rqx, dy = s8y - rqy;
+            pass &= !(fmaf(dy, dy, dx * dx) > rho2);
+        }
+        (void)pass_all;
+        /* the exact discriminant (isect) */
+        const float ocx = o[0] - s[0], ocy = o[1] - s[1], ocz = o[2] - s[2];
+        const float b = fmaf(ocz, d[2], fmaf(ocy, d[1], ocx * d[0]));
+        const float qx = fmaf(-b, d[0], ocx);
+        const float qy = fmaf(-b, d[1], ocy);
+        const float qz = fmaf(-b, d[2], ocz);
+        const float qq = fmaf(qz, qz, fmaf(qy, qy, qx * qx));
+        const float h = fmaf(s[3], s[3], -qq);
+        const int exact = !(h < 0.0f);
+        out[0] += (uint64_t)(exact && !pass);
+        out[1] += (uint64_t)pass;
+        out[2] += (uint64_t)exact;
+    }
+}
+
 /* Test-only: the product's light-plane shadow screen (rt_kernels.hip walk<>,
  * shd_screen_kernel; rt_capi.cpp do_render makes the basis) against the
  * exact discriminant of isect, for m (origin, sphere) pairs with the

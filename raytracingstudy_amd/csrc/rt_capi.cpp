@@ -38,6 +38,8 @@ hipError_t launch_shd_screen(const float4* prim_sp, uint32_t n, const float e[6]
                              float4* out, float2* out8, uint32_t* rr_max, hipStream_t st);
 hipError_t launch_albedo_refs(const uint32_t* prim_idx, const uint32_t* albedo, uint32_t n,
                               uint32_t n_spheres, uint32_t* out, hipStream_t st);
+hipError_t launch_cam8_screen(const float4* prim_sp, uint32_t n, const float o[3], const float B[9],
+                              uint32_t ok, float2* out, hipStream_t st);
 }  // namespace rtamd
 
 using namespace rtamd;
@@ -200,6 +202,11 @@ struct rt_renderer {
     DevBuf<float2> d_prim_shd8;
     DevBuf<uint32_t> d_shd_rr;
     float shd_rr = 0.0f;
+    // image-plane screen records (SceneArgs::prim_cam8) and what they were
+    // made for: the scene, the camera origin and the basis (with its check)
+    DevBuf<float2> d_prim_cam8;
+    uint64_t cam8_gen = ~0ull;
+    float cam8_key[13] = {};
     // albedo by leaf reference (SceneArgs::prim_al) and the scene it was made for
     DevBuf<uint32_t> d_prim_al;
     uint64_t al_gen = ~0ull;
@@ -771,6 +778,58 @@ int poison_outputs(rt_renderer* r, const FrameArgs& a, hipStream_t st) {
     return RT_OK;
 }
 
+// The image-plane screen's basis (SceneArgs::prim_cam8, DESIGN.md 5.1 round
+// 6): rows x, y, z, orthonormal in f64 and rounded to f32, z along the ray
+// through the image centre (getRay's K and R, include/camera.h:24-41).
+// Returns 1 when every primary ray of the W x H frame keeps (B d).z >= 0.1
+// |B d| (checked at the image corners: the rays' directions are the cone
+// they span, and the ratio is kept under positive combinations), else 0:
+// the records then pass every sphere.
+uint32_t cam8_basis(const FrameArgs& a, float B[9]) {
+    auto ray = [&](double u, double v, double w[3]) {
+        const double dx = (u - a.cam.K[2]) / a.cam.K[0], dy = (v - a.cam.K[5]) / a.cam.K[4];
+        for (int i = 0; i < 3; ++i) w[i] = a.cam.R[i] * dx + a.cam.R[3 + i] * dy + a.cam.R[6 + i];
+    };
+    double z[3], x[3] = {a.cam.R[0], a.cam.R[1], a.cam.R[2]}, y[3];
+    ray(0.5 * a.W, 0.5 * a.H, z);
+    const double zn = sqrt(z[0] * z[0] + z[1] * z[1] + z[2] * z[2]);
+    if (!(zn > 0.0) || !std::isfinite(zn)) {
+        for (int i = 0; i < 9; ++i) B[i] = i % 4 == 0 ? 1.0f : 0.0f;
+        return 0u;
+    }
+    for (double& t : z) t /= zn;
+    const double xz = x[0] * z[0] + x[1] * z[1] + x[2] * z[2];
+    for (int i = 0; i < 3; ++i) x[i] -= xz * z[i];
+    double xn = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+    if (!(xn > 1e-3)) {  // R's first column along the view: any perpendicular
+        x[0] = fabs(z[0]) < 0.9 ? 1.0 : 0.0;
+        x[1] = fabs(z[0]) < 0.9 ? 0.0 : 1.0;
+        x[2] = 0.0;
+        const double t = x[0] * z[0] + x[1] * z[1];
+        for (int i = 0; i < 3; ++i) x[i] -= t * z[i];
+        xn = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+    }
+    for (double& t : x) t /= xn;
+    y[0] = z[1] * x[2] - z[2] * x[1];
+    y[1] = z[2] * x[0] - z[0] * x[2];
+    y[2] = z[0] * x[1] - z[1] * x[0];
+    for (int i = 0; i < 3; ++i) {
+        B[i] = static_cast<float>(x[i]);
+        B[3 + i] = static_cast<float>(y[i]);
+        B[6 + i] = static_cast<float>(z[i]);
+    }
+    uint32_t ok = 1u;
+    for (int k = 0; k < 4; ++k) {
+        double w[3], p[3];
+        ray((k & 1) ? a.W : 0.0, (k & 2) ? a.H : 0.0, w);
+        for (int i = 0; i < 3; ++i)
+            p[i] = (double)B[3 * i] * w[0] + (double)B[3 * i + 1] * w[1] + (double)B[3 * i + 2] * w[2];
+        const double pn = sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]);
+        if (!(p[2] >= 0.1 * pn) || !std::isfinite(pn)) ok = 0u;
+    }
+    return ok;
+}
+
 int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : r->stream;
     if (r->cfg.mode == RT_MODE_SCENE && !r->has_scene)
@@ -834,6 +893,25 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
             r->cam_gen = r->scene_gen;
         }
         a.sc.prim_cam = r->d_prim_cam.p;
+        // the image-plane records of this frame's camera (origin, basis)
+        {
+            const uint32_t ok = cam8_basis(a, a.cam8_B);
+            float key[13];
+            memcpy(key, a.cam.o, sizeof(a.cam.o));
+            memcpy(key + 3, a.cam8_B, sizeof(a.cam8_B));
+            key[12] = ok ? 1.0f : 0.0f;
+            const float2* before8 = r->d_prim_cam8.p;
+            if ((ost = ensure(r, r->d_prim_cam8, nr))) return ost;
+            if (r->d_prim_cam8.p != before8 || r->cam8_gen != r->scene_gen ||
+                memcmp(r->cam8_key, key, sizeof(key)) != 0) {
+                hipError_t e = launch_cam8_screen(a.sc.prim_sp, nr, a.cam.o, a.cam8_B, ok,
+                                                  r->d_prim_cam8.p, st);
+                if (e != hipSuccess) return hip_fail(r, e, "image-plane screen records");
+                memcpy(r->cam8_key, key, sizeof(key));
+                r->cam8_gen = r->scene_gen;
+            }
+            a.sc.prim_cam8 = r->d_prim_cam8.p;
+        }
         // the light-plane screen: an orthonormal basis {e1, e2} of the plane
         // perpendicular to the shadow direction a.L (in f64 from the f32 L the
         // kernel uses, then rounded), and the records of its centres, remade
@@ -1140,6 +1218,7 @@ int rt_destroy(rt_renderer* r) {
     r->d_albedo.release();
     r->d_prim_cam.release();
     r->d_prim_al.release();
+    r->d_prim_cam8.release();
     r->d_prim_shd8.release();
     r->d_shd_rr.release();
     r->d_prim_shd.release();

@@ -294,6 +294,29 @@ constexpr bool kLdsShadow = RT_LDS_SHADOW != 0;
 #ifndef RT_SHD8
 #define RT_SHD8 1
 #endif
+// Image-plane screen for primary rays in 8 bytes (SceneArgs::prim_cam8,
+// DESIGN.md 5.1 round 6): the primary walks screen a chunk's two spheres
+// from ONE dwordx4 instead of two 16-byte camera-relative records, and stage
+// no leaves in LDS.  C3 -2.9%, C5 -2.4%, C5d -2.1%, C2 -1.9% (unsorted and
+// sorted walks, profiles/r06/ab_cam8_sorted.log); RT_CAM8=0: the 16-byte
+// camera-relative screen and its LDS staging
+#ifndef RT_CAM8
+#define RT_CAM8 1
+#endif
+// ... LDS staging of the 8-byte records, pairs per float4, from
+// kLdsLeafMin8 spheres: C3 +1.2 / +1.3 / +3.4% from 8 / 5 / 3 against none
+// (ab_cam8_staging.log), so off
+#ifndef RT_CAM8_LDS
+#define RT_CAM8_LDS 0
+#endif
+// ... for the sorted walks (C5, C5d) too
+#ifndef RT_CAM8_SORTED
+#define RT_CAM8_SORTED 1
+#endif
+#ifndef RT_CAM8_LDS_MIN
+#define RT_CAM8_LDS_MIN 5
+#endif
+constexpr uint32_t kLdsLeafMin8 = RT_CAM8_LDS_MIN;
 // spheres per chunk of the shadow walks (with 8-byte records: two per dwordx4);
 // 4 spills 48-100 B and runs C3 +6%, C5 +8%, C5d +5% (profiles/r06/ab_shd_chunk4.log)
 #ifndef RT_SHD_CHUNK
@@ -370,7 +393,7 @@ __device__ __forceinline__ bool glds_leaf(const float4* src, float4* dst, uint32
 // any-hit walk (a per-lane direction: ambient occlusion, area lights) keeps
 // the full discriminant screen.
 template <bool kAnyHitT, int kChunk = 2, bool kDynAny = false, bool kStats = true,
-          bool kNoStack = false, bool kShadowL = false>
+          bool kNoStack = false, bool kShadowL = false, bool kCam8 = false>
 __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, float o2, float d0,
                                      float d1, float d2, float tmin, float tmax, float& tout,
                                      uint32_t& iout, uint32_t& n_nodes, uint32_t& n_prims,
@@ -389,6 +412,19 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
     // Shadow (any-hit) walks start at hit points and keep the full screen.
     const bool cam = kCamMode != 0 && !kAnyHit;
     const bool cam_exact = cam && kCamMode == 2;  // records {o - c, r}: the tests use them as they are
+    // 8-byte image-plane records (RT_CAM8, unsorted nearest walks): the
+    // lane's point s = (Bd).xy / (Bd).z, once per walk
+    const bool cam8 = kCam8 && cam && !cam_exact && kChunk % 2 == 0;
+    float s8x = 0.0f, s8y = 0.0f;
+    if (cam8) {
+        KernArgs* kb = kernargs();
+        const float px = fmaf(kb->cam8_B[2], d2, fmaf(kb->cam8_B[1], d1, kb->cam8_B[0] * d0));
+        const float py = fmaf(kb->cam8_B[5], d2, fmaf(kb->cam8_B[4], d1, kb->cam8_B[3] * d0));
+        const float pz = fmaf(kb->cam8_B[8], d2, fmaf(kb->cam8_B[7], d1, kb->cam8_B[6] * d0));
+        const float iz = __builtin_amdgcn_rcpf(pz);
+        s8x = px * iz;
+        s8y = py * iz;
+    }
     // Light-plane screen: a shadow walk's direction is the
     // frame's L in every lane, so a sphere is near the ray iff its centre is
     // near the ray's origin in the plane perpendicular to L.  The records
@@ -403,6 +439,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
     float up = 0.0f, vp = 0.0f;
     const bool shd8 = RT_SHD8 && kChunk % 2 == 0 && shd;
     const float2* __restrict__ shd8_base = shd8 ? S.prim_shd8 : nullptr;
+    const float2* __restrict__ cam8_base = cam8 ? kernargs()->sc.prim_cam8 : nullptr;
     const float shd_rr = shd8 ? kernargs()->shd_rr : 0.0f;
     if (shd) {
         KernArgs* ke = kernargs();
@@ -484,7 +521,9 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
     // oracle): each lane loads its own, kChunk loads in flight.
     // The chunk loop over one leaf's spheres (offset off, count cnt), each
     // read as load(k), k counted from the leaf's first reference.
-    auto chunks = [&](auto&& load, uint32_t off, uint32_t cnt) -> bool {
+    // plb: with 8-byte image-plane records staged in LDS (RT_CAM8_LDS), the
+    // wave's buffer, pairs of records per float4; ~0u: records from global
+    auto chunks = [&](auto&& load, uint32_t off, uint32_t cnt, uint32_t plb = ~0u) -> bool {
         // cnt >= 1 (a leaf is a non-empty cell; the root leaf is guarded by
         // its caller): a do-while skips the loop-entry test and its branch
         uint32_t j = 0;
@@ -507,12 +546,16 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             // costs the texture path as much for one lane as for 64, and at
             // a leaf's odd end the whole wave usually has no slot 1
             bool fetched[kChunk];
-            if (shd8) {
-                // two slots' {u, v} per dwordx4 (8-byte aligned: global loads
-                // need dword alignment only; shd8 implies an even kChunk)
+            if (shd8 || cam8) {
+                // two slots' 8-byte records per dwordx4 (8-byte aligned:
+                // global loads need dword alignment only; an even kChunk)
 #pragma unroll
                 for (int h = 0; h < kChunk / 2; ++h) {
-                    const float4 pr = *reinterpret_cast<const float4*>(shd8_base + (off + j + 2u * h));
+                    extern __shared__ __attribute__((aligned(16))) float4 lds_pairs[];
+                    const float4 pr = cam8 && plb != ~0u
+                                          ? lds_pairs[plb + (j >> 1) + h]
+                                          : *reinterpret_cast<const float4*>((cam8 ? cam8_base : shd8_base) +
+                                                                             (off + j + 2u * h));
                     sv[2 * h] = make_float4(pr.x, pr.y, 0.0f, 0.0f);
                     sv[2 * h + 1] = make_float4(pr.z, pr.w, 0.0f, 0.0f);
                     fetched[2 * h] = fetched[2 * h + 1] = true;
@@ -547,6 +590,13 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                 bool pos;
                 if (cam_exact) {
                     pos = !(isect_h_oc(sv[q].x, sv[q].y, sv[q].z, d0, d1, d2, sv[q].w) < 0.0f);
+                } else if (cam8) {
+                    // the lane's image-plane distance from the centre's
+                    // projection against rho^2 (bf16 in the records' low bytes)
+                    const float rho2 = __uint_as_float(__builtin_amdgcn_perm(
+                        __float_as_uint(sv[q].x), __float_as_uint(sv[q].y), 0x04000C0Cu));
+                    const float dx = s8x - sv[q].x, dy = s8y - sv[q].y;
+                    pos = !(fmaf(dy, dy, dx * dx) > rho2);
                 } else if (cam) {
                     // b exactly as isect computes it ({x,y,z} = o - c in the
                     // same f32 operations); C' undercuts |o-c|^2 - r^2 by the
@@ -570,7 +620,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             if (j + 1u >= cnt) RT_BS(kBsPastEnd);
 #endif
             if (__builtin_expect(__any(maybe), 0)) {
-                if ((cam && !cam_exact) || shd) {  // the exact tests need the spheres themselves
+                if ((cam && !cam_exact) || shd) {  // the exact tests need the spheres themselves (cam8 too)
                     RT_BS(kBsExactLoad);
                     const float4* __restrict__ ex = kernargs()->sc.prim_sp + off;
 #pragma unroll
@@ -601,7 +651,7 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
         // the exact tests skip as before.
         const uint32_t off_u = __builtin_amdgcn_readfirstlane(off);
         const uint32_t cnt_u = __builtin_amdgcn_readfirstlane(cnt);
-        if ((kLdsShadow || !kAnyHit) && cnt_u >= kLdsLeafMin && cnt_u < kernargs()->sc.lds_max &&
+        if ((kLdsShadow || !kAnyHit) && !cam8 && cnt_u >= kLdsLeafMin && cnt_u < kernargs()->sc.lds_max &&
             __all(off == off_u)) {
             RT_BS(kBsLdsLeaf);
             extern __shared__ __attribute__((aligned(16))) float4 lds_leaf[];
@@ -616,6 +666,20 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
             // (a wave's LDS operations complete in order: the reads below see
             // the writes, and the compiler keeps them in order: same array)
             return chunks([&](uint32_t k) { return lds_leaf[lb + k]; }, off_u, cnt_u);
+        }
+        // the same for 8-byte image-plane records: pairs of records, one
+        // float4 per active lane, the chunks reading a pair per ds_read_b128
+        if (RT_CAM8_LDS && cam8 && cnt_u >= kLdsLeafMin8 && cnt_u < 2u * kernargs()->sc.lds_max &&
+            __all(off == off_u)) {
+            RT_BS(kBsLdsLeaf);
+            extern __shared__ __attribute__((aligned(16))) float4 lds_leaf[];
+            const uint32_t lb = lb_u != ~0u ? lb_u : leaf_buf_base(S, kNoStack);
+            const float4* __restrict__ pu = reinterpret_cast<const float4*>(cam8_base + off_u);
+            const uint32_t np = (cnt_u + 1u) >> 1;  // pairs (an odd leaf's last pair reads one past it)
+            const uint64_t act = __ballot(1);
+            const uint32_t na = static_cast<uint32_t>(__popcll(act));
+            for (uint32_t k = lane_rank(act); k < np; k += na) lds_leaf[lb + k] = pu[k];
+            return chunks([&](uint32_t k) { return lds_leaf[lb + k]; }, off_u, cnt_u, lb);
         }
 #endif
         const float4* __restrict__ ps = prim_sp + off;
@@ -874,7 +938,7 @@ __device__ __forceinline__ uint32_t hit_albedo(SA& S, uint32_t h) {
 
 // Unified lane path: one walk instance run twice (primary, then the shadow ray
 // of the lanes that need one), so the register allocator sees one walk.
-template <int kChunk, bool kStats>
+template <int kChunk, bool kStats, bool kCam8 = false>
 __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uint32_t x,
                                                          uint32_t y, uint32_t hp, uint32_t s,
                                                          bool valid, uint32_t& n_shadow,
@@ -911,7 +975,7 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
             RT_BS(kBsPhase);
             if (phase) RT_BS(kBsPhaseShadow);
             if (phase == 0)
-                hit = walk<false, kChunk, false, kStats>(S, r0, r1, r2, d0, d1, d2, 0.0f, INFINITY, t,
+                hit = walk<false, kChunk, false, kStats, false, false, kCam8>(S, r0, r1, r2, d0, d1, d2, 0.0f, INFINITY, t,
                                                          idx, n_nodes, n_prims,
                                                          static_cast<uint2*>(stk), false, bs, lbs);
             else {
@@ -974,7 +1038,7 @@ __device__ __forceinline__ PixelOut sample_color_unified(const FrameArgs& a, uin
 // live across the walks instead of the slot and the tile-local origin).
 // Rounds of spw samples, pairwise butterfly per round, rounds added in
 // order in the leader's LDS slot, then the mean is written.
-template <bool kTiles, int kChunk, bool kStats, bool kProg>
+template <bool kTiles, int kChunk, bool kStats, bool kProg, bool kCam8 = false>
 __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc, void* stk,
                                                 uint32_t ox, uint32_t oy, uint32_t obase,
                                                 uint32_t& n_primary,
@@ -1002,7 +1066,7 @@ __device__ __forceinline__ void shade_wave_tile(const FrameArgs& a, float4* acc,
         const uint32_t sg = r * spw + sub_base;
         const bool valid = lane_ok && sg < s_end;
         n_primary += static_cast<uint32_t>(__popcll(__ballot(valid)));  // wave-uniform
-        PixelOut c = sample_color_unified<kChunk, kStats>(a, x, y, hp, sg, valid, n_shadow,
+        PixelOut c = sample_color_unified<kChunk, kStats, kCam8>(a, x, y, hp, sg, valid, n_shadow,
                                                           n_nodes, n_prims, stk, bs, lbs);
         // Pixel sum of this round: pairwise butterfly over the pixel's g
         // lanes (missing samples are 0) = oracle.c:tree_sum; rounds are then
@@ -1180,7 +1244,7 @@ __device__ __forceinline__ void shade_pixel_sorted(const FrameArgs& a, float* wl
         if (valid) {
             RT_BS(kBsPhase);
             KernArgs* kc = kernargs();
-            hit = walk<false, kChunk, true, kStats, true>(S, kc->cam.o[0], kc->cam.o[1], kc->cam.o[2],
+            hit = walk<false, kChunk, true, kStats, true, false, RT_CAM8_SORTED != 0>(S, kc->cam.o[0], kc->cam.o[1], kc->cam.o[2],
                                                           d0, d1, d2, 0.0f, INFINITY, t, idx, n_nodes,
                                                           n_prims, static_cast<uint2*>(stk), false, bs,
                                                           lbs);
@@ -1526,7 +1590,7 @@ __device__ __forceinline__ void scene_body(FrameArgs a) {
                     shade_pixel_sorted<kTiles, kChunk, kStats, kProg>(
                         a, wl, stk, ox, oy, obase, n_primary, n_shadow, n_nodes, n_prims, bs, lbs);
                 else
-                    shade_wave_tile<kTiles, kChunk, kStats, kProg>(
+                    shade_wave_tile<kTiles, kChunk, kStats, kProg, RT_CAM8 != 0 && !kSort>(
                         a, acc, stk, ox, oy, obase, n_primary, n_shadow, n_nodes, n_prims, bs, lbs);
 #ifdef RT_TIMELINE
                 // per unit {start, end, hw_id << 32 | xcc << 16 | wave index}
@@ -1693,6 +1757,74 @@ hipError_t launch_cam_screen(const float4* prim_sp, uint32_t n, const float o[3]
     if (n) {
         hipLaunchKernelGGL(cam_screen_kernel, dim3((n + kBlockThreads - 1) / kBlockThreads),
                            dim3(kBlockThreads), 0, st, prim_sp, n, o[0], o[1], o[2], out);
+    }
+    return hipGetLastError();
+}
+
+// Image-plane screen records (SceneArgs::prim_cam8).
+// For basis B (f32 rows, orthonormal to f32 rounding) and camera origin o,
+// a sphere's centre direction a = B(c - o)/|c - o| projects to q = a.xy/a.z.
+// A ray the exact test accepts passes within r' = r (1 + 1e-6) of c, so its
+// direction b is within theta (sin theta = r'/|c - o|) of a, and for unit
+// vectors |q_a - q_b| <= |a x b| / (a_z b_z) <= sin theta / (a_z cos(beta +
+// theta)), beta the angle of a from B's z axis.  rho adds the f32 errors of
+// the lane's point (4e-6 (1 + |q| + rho)^2, ~5x the bound), the stored
+// centre's (its 8 low mantissa bits carry rho^2: <= 2^-14 |q| a component)
+// and 1e-5 relative; rho^2 is rounded up to bf16.  Spheres near or behind
+// the camera plane, or a frame whose rays B does not keep in front (ok = 0),
+// get rho^2 = +inf: always passed.
+__global__ void __launch_bounds__(kBlockThreads)
+    cam8_screen_kernel(const float4* __restrict__ prim_sp, uint32_t n, float ox, float oy, float oz,
+                       float b0, float b1, float b2, float b3, float b4, float b5, float b6, float b7,
+                       float b8, uint32_t ok, float2* __restrict__ out) {
+    const uint32_t i = blockIdx.x * kBlockThreads + threadIdx.x;
+    if (i >= n) return;
+    const float4 c = prim_sp[i];
+    const double vx = static_cast<double>(c.x) - ox, vy = static_cast<double>(c.y) - oy,
+                 vz = static_cast<double>(c.z) - oz;
+    const double X = static_cast<double>(b0) * vx + static_cast<double>(b1) * vy + static_cast<double>(b2) * vz;
+    const double Y = static_cast<double>(b3) * vx + static_cast<double>(b4) * vy + static_cast<double>(b5) * vz;
+    const double Z = static_cast<double>(b6) * vx + static_cast<double>(b7) * vy + static_cast<double>(b8) * vz;
+    const double dist = sqrt(vx * vx + vy * vy + vz * vz);
+    const double rp = static_cast<double>(c.w) * (1.0 + 1e-6);
+    uint32_t hx = 0u, hy = 0u, rb = 0x7F800000u;  // rho^2 = +inf: always pass
+    bool pass_all = !ok || !(dist > rp * 1.0001) || !(Z > 0.0) || !isfinite(dist) || !(c.w >= 0.0f);
+    if (!pass_all) {
+        const double az = Z / dist;
+        const double beta = acos(fmin(1.0, az));
+        const double th = asin(fmin(1.0, rp / dist));
+        if (!(beta + th < 1.45)) {  // ~83 degrees: the bound's cos(beta + theta) too small
+            pass_all = true;
+        } else {
+            const float qx = static_cast<float>(X / Z), qy = static_cast<float>(Y / Z);
+            const double q = fabs(static_cast<double>(qx)) + fabs(static_cast<double>(qy));
+            const double rho_g = sin(th) / (az * cos(beta + th));
+            const double eps_c = 1.5 * (1.0 / 16384.0) * q;
+            const double m = 1.0 + q + rho_g;
+            const double rho = rho_g * (1.0 + 1e-5) + eps_c + 4e-6 * m * m;
+            const float r2 = __double2float_ru(rho * rho * (1.0 + 1e-6));
+            uint32_t bits = __float_as_uint(r2);
+            if (bits & 0xFFFFu) bits = (bits & 0xFFFF0000u) + 0x10000u;  // bf16, rounded up
+            if (isfinite(r2) && bits < 0x7F800000u) {
+                rb = bits;
+                hx = __float_as_uint(qx);
+                hy = __float_as_uint(qy);
+            } else {
+                pass_all = true;
+            }
+        }
+    }
+    // low bytes: rho^2's bf16, high byte in x, low byte in y
+    const uint32_t sx = (hx & ~0xFFu) | (rb >> 24), sy = (hy & ~0xFFu) | ((rb >> 16) & 0xFFu);
+    out[i] = make_float2(__uint_as_float(sx), __uint_as_float(sy));
+}
+
+hipError_t launch_cam8_screen(const float4* prim_sp, uint32_t n, const float o[3], const float B[9],
+                              uint32_t ok, float2* out, hipStream_t st) {
+    if (n) {
+        hipLaunchKernelGGL(cam8_screen_kernel, dim3((n + kBlockThreads - 1) / kBlockThreads),
+                           dim3(kBlockThreads), 0, st, prim_sp, n, o[0], o[1], o[2], B[0], B[1], B[2],
+                           B[3], B[4], B[5], B[6], B[7], B[8], ok, out);
     }
     return hipGetLastError();
 }

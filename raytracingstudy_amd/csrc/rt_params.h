@@ -201,6 +201,12 @@ struct SceneArgs {
     // dwordx4 carries a chunk's two; the radius term is the scene's largest
     // rr' (FrameArgs::shd_rr), so the screen passes a superset still
     const float2* prim_shd8;
+    // Image-plane screen records of primary rays in 8 bytes (RT_CAM8): per
+    // reference {qx, qy}, the sphere centre's gnomonic projection in the
+    // basis FrameArgs::cam8_B, with a bf16 bound rho^2 on the image-plane
+    // distance of every ray the exact test may accept folded into the low
+    // bytes (cam8_screen_kernel); one dwordx4 a chunk
+    const float2* prim_cam8;
     // Albedo by leaf reference (albedo[prim_idx[ref]], made once per scene,
     // albedo_refs_kernel): a nearest walk returns its hit's REFERENCE, and the
     // hit is shaded from prim_sp[ref] and prim_al[ref], lines the walk's own
@@ -242,6 +248,7 @@ struct FrameArgs {
     float L[3];         // unit vector toward the light
     float shd_e[6];     // light-plane basis {e1, e2} (orthonormal, perpendicular to L; f32)
     float shd_rr;       // the largest light-plane rr' of the scene (SceneArgs::prim_shd8)
+    float cam8_B[9];    // orthonormal basis of the image-plane screen, rows x, y, z (f32)
     float ambient;
     float inv_spp;      // 1 / samples in the image (all accumulated frames)
     // progressive accumulation (RT_FLAG_PROGRESSIVE)
