@@ -938,7 +938,8 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
         const float2* before_s8 = r->d_prim_shd8.p;
         if ((ost = ensure(r, r->d_prim_shd, nr))) return ost;
         if ((ost = ensure(r, r->d_prim_shd8, nr))) return ost;
-        if ((ost = ensure(r, r->d_shd_rr, 1))) return ost;
+        const uint32_t nbk = (nr + kBlockThreads - 1u) / kBlockThreads;  // shd_screen_kernel's blocks
+        if ((ost = ensure(r, r->d_shd_rr, nbk + 1u))) return ost;
         if (r->d_prim_shd.p != before_s || r->d_prim_shd8.p != before_s8 || r->shd_gen != r->scene_gen ||
             memcmp(r->shd_e, a.shd_e, sizeof(r->shd_e)) != 0) {
             // M bounds |origin| and |centre| of every shadow test: the root
@@ -954,13 +955,13 @@ int do_render(rt_renderer* r, FrameArgs& a, void* stream, rt_stats* stats) {
                 m = std::max(m, sqrt(q));
             }
             const double delta = kShadowSlackM / 16777216.0 * (m + 1e-4);
-            RT_HIP(r, hipMemsetAsync(r->d_shd_rr.p, 0, sizeof(uint32_t), st));
+            RT_HIP(r, hipMemsetAsync(r->d_shd_rr.p, 0, (nbk + 1u) * sizeof(uint32_t), st));
             hipError_t e = launch_shd_screen(a.sc.prim_sp, nr, a.shd_e, delta, r->d_prim_shd.p,
                                              r->d_prim_shd8.p, r->d_shd_rr.p, st);
             if (e != hipSuccess) return hip_fail(r, e, "light-plane screen records");
             // the 8-byte records' radius term, once per scene and light (a sync)
             uint32_t bits = 0;
-            RT_HIP(r, hipMemcpyAsync(&bits, r->d_shd_rr.p, sizeof(bits), hipMemcpyDeviceToHost, st));
+            RT_HIP(r, hipMemcpyAsync(&bits, r->d_shd_rr.p + nbk, sizeof(bits), hipMemcpyDeviceToHost, st));
             RT_HIP(r, hipStreamSynchronize(st));
             memcpy(&r->shd_rr, &bits, sizeof(bits));
             memcpy(r->shd_e, a.shd_e, sizeof(r->shd_e));

@@ -1741,19 +1741,45 @@ __global__ void __launch_bounds__(kBlockThreads)
     if (out8) {
         // the largest rr' (non-negative floats order as their bits; a NaN
         // radius, the test-only pad fill, orders above every number): the
-        // wave's maximum first, then one atomic per wave (one per thread
-        // took C5d's 4.9 M records 0.87 ms on a single word)
+        // block's maximum into rr_max[blockIdx.x], reduced by
+        // max_bits_kernel (atomics on one word serialise across the XCDs:
+        // one per record, or one per wave, took C5d's 4.9 M records 0.87 ms)
+        __shared__ uint32_t wmax[kBlockThreads / 64];
         for (int d = 32; d > 0; d >>= 1) rb = max(rb, static_cast<uint32_t>(__shfl_xor(static_cast<int>(rb), d, 64)));
-        if ((threadIdx.x & 63u) == 0u && rb) atomicMax(rr_max, rb);
+        if ((threadIdx.x & 63u) == 0u) wmax[threadIdx.x >> 6] = rb;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t m = 0u;
+            for (uint32_t w = 0; w < kBlockThreads / 64; ++w) m = max(m, wmax[w]);
+            rr_max[blockIdx.x] = m;
+        }
+    }
+}
+
+// out[0] = the largest of in[0 .. n) (one block)
+__global__ void __launch_bounds__(kBlockThreads)
+    max_bits_kernel(const uint32_t* __restrict__ in, uint32_t n, uint32_t* __restrict__ out) {
+    __shared__ uint32_t wmax[kBlockThreads / 64];
+    uint32_t m = 0u;
+    for (uint32_t i = threadIdx.x; i < n; i += kBlockThreads) m = max(m, in[i]);
+    for (int d = 32; d > 0; d >>= 1) m = max(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), d, 64)));
+    if ((threadIdx.x & 63u) == 0u) wmax[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint32_t w = 1; w < kBlockThreads / 64; ++w) m = max(m, wmax[w]);
+        out[0] = m;
     }
 }
 
 hipError_t launch_shd_screen(const float4* prim_sp, uint32_t n, const float e[6], double delta,
                              float4* out, float2* out8, uint32_t* rr_max, hipStream_t st) {
+    // rr_max: (blocks + 1) words, the scene's largest rr' bits in the last
     if (n) {
-        hipLaunchKernelGGL(shd_screen_kernel, dim3((n + kBlockThreads - 1) / kBlockThreads),
-                           dim3(kBlockThreads), 0, st, prim_sp, n, e[0], e[1], e[2], e[3], e[4], e[5],
-                           delta, out, out8, rr_max);
+        const uint32_t nb = (n + kBlockThreads - 1) / kBlockThreads;
+        hipLaunchKernelGGL(shd_screen_kernel, dim3(nb), dim3(kBlockThreads), 0, st, prim_sp, n, e[0],
+                           e[1], e[2], e[3], e[4], e[5], delta, out, out8, rr_max);
+        if (out8)
+            hipLaunchKernelGGL(max_bits_kernel, dim3(1), dim3(kBlockThreads), 0, st, rr_max, nb, rr_max + nb);
     }
     return hipGetLastError();
 }
