@@ -127,7 +127,10 @@ def test_lds_staging_on_and_off(gpu, oracle, case, monkeypatch):
     """LDS leaf staging changes which path reads a leaf's spheres, never what
     a frame computes: on (the default) and off (RT_LDS_STAGE=0, read when
     the scene is built), plain and stats frames give the oracle's image and
-    counters."""
+    counters.  (Since the 8-byte screens, RT_CAM8, the default build's walks
+    stage no leaves, so here both settings read globally; the staging path
+    is what RT_CAM8=0 builds run, parity-checked when they were the default,
+    profiles/r06/pytest_*.log.)"""
     n, w, h, spp, depth = case
     sp, al = rt.generate_spheres(n, rt.SEED)
     out = {}
