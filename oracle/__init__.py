@@ -56,6 +56,8 @@ def load() -> ctypes.CDLL:
         "orc_max_threads": (ctypes.c_int, []),
         "orc_cam_screen_check": (None, [_P, _P, _P, _P, _u32, ctypes.c_double, ctypes.c_double, _P]),
         "orc_cam8_screen_check": (None, [_P, _P, _u32, _P, _P, _P, _u32, ctypes.c_double, _P]),
+        "orc_shd8_screen_check": (None, [_P, _P, _P, _P, _u32, ctypes.c_double, ctypes.c_double,
+                                         ctypes.c_double, ctypes.c_double, _P]),
         "orc_shd_screen_check": (None, [_P, _P, _P, _P, _u32, ctypes.c_double, ctypes.c_double,
                                         ctypes.c_double, _P]),
     }
@@ -228,6 +230,22 @@ def cam8_screen_check(o, B, ok: int, dirs, spheres, idx, shrink: float = 1.0):
     out = np.zeros(3, np.uint64)
     load().orc_cam8_screen_check(_p(oa), _p(ba), int(ok), _p(d), _p(sp), _p(ix), d.shape[0],
                                  float(shrink), _p(out))
+    return int(out[0]), int(out[1]), int(out[2])
+
+
+def shd8_screen_check(origins, L, spheres, idx, big_m: float, slack_m: float, grow: float,
+                      shrink: float = 1.0):
+    """Test-only check of the light-plane screen with per-sphere radii packed
+    into 8-byte records (oracle.c orc_shd8_screen_check): (exact-accepted
+    pairs the screen rejects, pairs passed, pairs the exact test accepts)."""
+    o = np.ascontiguousarray(origins, np.float32).reshape(-1, 3)
+    la = _f32(L, 3)
+    sp = np.ascontiguousarray(spheres, np.float32).reshape(-1, 4)
+    ix = np.ascontiguousarray(idx, np.uint32).reshape(-1)
+    assert ix.shape[0] == o.shape[0]
+    out = np.zeros(3, np.uint64)
+    load().orc_shd8_screen_check(_p(o), _p(la), _p(sp), _p(ix), o.shape[0], float(big_m),
+                                 float(slack_m), float(grow), float(shrink), _p(out))
     return int(out[0]), int(out[1]), int(out[2])
 
 

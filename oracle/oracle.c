@@ -598,6 +598,79 @@ void orc_cam8_screen_check(const float o[3], const float B[9], uint32_t ok, cons
     }
 }
 
+/* Test-only: the light-plane screen with 8-byte records carrying each
+ * sphere's own rr' as bf16 in the low bytes of {u, v} (rt_kernels.hip
+ * shd_screen_kernel and walk<> under RT_SHD8_PER): as orc_shd_screen_check,
+ * the radius grown by the stored centre's error 2^-14 (|u| + |v|) and the
+ * result scaled by shrink (1 = the product). */
+void orc_shd8_screen_check(const float* origins, const float L[3], const float* sp,
+                           const uint32_t* idx, uint32_t m, double big_m, double slack_m,
+                           double grow, double shrink, uint64_t out[3]) {
+    const double u = 1.0 / 16777216.0;
+    double l[3] = {L[0], L[1], L[2]};
+    const double ln = sqrt(l[0] * l[0] + l[1] * l[1] + l[2] * l[2]);
+    for (int i = 0; i < 3; ++i) l[i] /= ln;
+    int kmin = 0;
+    for (int i = 1; i < 3; ++i)
+        if (fabs(l[i]) < fabs(l[kmin])) kmin = i;
+    double e1[3] = {0.0, 0.0, 0.0};
+    e1[kmin] = 1.0;
+    const double al = l[kmin];
+    for (int i = 0; i < 3; ++i) e1[i] -= al * l[i];
+    const double n1 = sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+    for (int i = 0; i < 3; ++i) e1[i] /= n1;
+    const double e2[3] = {l[1] * e1[2] - l[2] * e1[1], l[2] * e1[0] - l[0] * e1[2],
+                          l[0] * e1[1] - l[1] * e1[0]};
+    float e[6];
+    for (int i = 0; i < 3; ++i) {
+        e[i] = (float)e1[i];
+        e[3 + i] = (float)e2[i];
+    }
+    const double delta = slack_m * u * (big_m + 1e-4);
+    out[0] = out[1] = out[2] = 0;
+    for (uint32_t k = 0; k < m; ++k) {
+        const float* o = origins + 3u * k;
+        const float* s = sp + 4u * idx[k];
+        const float ocx = o[0] - s[0], ocy = o[1] - s[1], ocz = o[2] - s[2];
+        const float b = fmaf(ocz, L[2], fmaf(ocy, L[1], ocx * L[0]));
+        const float qx = fmaf(-b, L[0], ocx);
+        const float qy = fmaf(-b, L[1], ocy);
+        const float qz = fmaf(-b, L[2], ocz);
+        const float qq = fmaf(qz, qz, fmaf(qy, qy, qx * qx));
+        const float h = fmaf(s[3], s[3], -qq);
+        /* the packed record (shd_screen_kernel) */
+        const double cu = (double)s[0] * e[0] + (double)s[1] * e[1] + (double)s[2] * e[2];
+        const double cv = (double)s[0] * e[3] + (double)s[1] * e[4] + (double)s[2] * e[5];
+        const float cuf = (float)cu, cvf = (float)cv;
+        const double ec = (1.0 / 16384.0) * (fabs((double)cuf) + fabs((double)cvf));
+        const double rg = ((double)s[3] * (1.0 + grow * u) + delta + ec) * shrink;
+        const double rr = rg * rg * (1.0 + grow * u);
+        float rrf = (float)rr;
+        if ((double)rrf < rr) rrf = nextafterf(rrf, INFINITY);
+        uint32_t rb, hu, hv;
+        memcpy(&rb, &rrf, 4);
+        if (rb & 0xFFFFu) rb = (rb & 0xFFFF0000u) + 0x10000u;
+        if (!(isfinite(rrf) && rb < 0x7F800000u)) rb = 0x7F800000u;
+        memcpy(&hu, &cuf, 4);
+        memcpy(&hv, &cvf, 4);
+        const uint32_t su = (hu & ~0xFFu) | (rb >> 24), sv = (hv & ~0xFFu) | ((rb >> 16) & 0xFFu);
+        float us, vs, rrd;
+        memcpy(&us, &su, 4);
+        memcpy(&vs, &sv, 4);
+        const uint32_t rbits = ((su & 0xFFu) << 24) | ((sv & 0xFFu) << 16);
+        memcpy(&rrd, &rbits, 4);
+        /* the lane */
+        const float up = fmaf(o[2], e[2], fmaf(o[1], e[1], o[0] * e[0]));
+        const float vp = fmaf(o[2], e[5], fmaf(o[1], e[4], o[0] * e[3]));
+        const float du = up - us, dv = vp - vs;
+        const int pass = !(fmaf(dv, dv, du * du) > rrd);
+        const int exact = !(h < 0.0f);
+        out[0] += (uint64_t)(exact && !pass);
+        out[1] += (uint64_t)pass;
+        out[2] += (uint64_t)exact;
+    }
+}
+
 /* Test-only: the product's light-plane shadow screen (rt_kernels.hip walk<>,
  * shd_screen_kernel; rt_capi.cpp do_render makes the basis) against the
  * exact discriminant of isect, for m (origin, sphere) pairs with the

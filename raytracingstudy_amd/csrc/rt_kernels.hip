@@ -317,6 +317,11 @@ constexpr bool kLdsShadow = RT_LDS_SHADOW != 0;
 #define RT_CAM8_LDS_MIN 5
 #endif
 constexpr uint32_t kLdsLeafMin8 = RT_CAM8_LDS_MIN;
+// ... each sphere's own rr' as bf16 in the records' low bytes (RT_SHD8_PER)
+// instead of the scene's largest
+#ifndef RT_SHD8_PER
+#define RT_SHD8_PER 0
+#endif
 // spheres per chunk of the shadow walks (with 8-byte records: two per dwordx4);
 // 4 spills 48-100 B and runs C3 +6%, C5 +8%, C5d +5% (profiles/r06/ab_shd_chunk4.log)
 #ifndef RT_SHD_CHUNK
@@ -607,7 +612,11 @@ __device__ __forceinline__ bool walk(const SceneArgs& S, float o0, float o1, flo
                     // the centre's light-plane distance from the origin; rr'
                     // covers the rounding, so every sphere isect accepts passes
                     const float du = up - sv[q].x, dv = vp - sv[q].y;
-                    pos = !(fmaf(dv, dv, du * du) > (shd8 ? shd_rr : sv[q].z));
+                    const float rr8 = RT_SHD8_PER ? __uint_as_float(__builtin_amdgcn_perm(
+                                                         __float_as_uint(sv[q].x), __float_as_uint(sv[q].y),
+                                                         0x04000C0Cu))
+                                                   : shd_rr;
+                    pos = !(fmaf(dv, dv, du * du) > (shd8 ? rr8 : sv[q].z));
                 } else {
                     pos = !(isect_h(o0, o1, o2, d0, d1, d2, sv[q]) < 0.0f);
                 }
@@ -1735,7 +1744,24 @@ __global__ void __launch_bounds__(kBlockThreads)
         const double rg = static_cast<double>(c.w) * (1.0 + 4.0 * ur) + delta;
         const float rr = __double2float_ru(rg * rg * (1.0 + 4.0 * ur));
         out[i] = make_float4(static_cast<float>(u), static_cast<float>(v), rr, 0.0f);
-        if (out8) out8[i] = make_float2(static_cast<float>(u), static_cast<float>(v));
+        if (out8) {
+            const float uf = static_cast<float>(u), vf = static_cast<float>(v);
+            if (RT_SHD8_PER) {
+                // this sphere's rr', grown by the stored centre's error (its
+                // 8 low mantissa bits a coordinate carry rr': <= 2^-15 |u|
+                // each), rounded up to bf16 (oracle.c orc_shd8_screen_check)
+                const double ec = (1.0 / 16384.0) * (fabs(static_cast<double>(uf)) + fabs(static_cast<double>(vf)));
+                const double rg8 = rg + ec;
+                const float r8 = __double2float_ru(rg8 * rg8 * (1.0 + 4.0 * ur));
+                uint32_t b8 = __float_as_uint(r8);
+                if (b8 & 0xFFFFu) b8 = (b8 & 0xFFFF0000u) + 0x10000u;
+                if (!(isfinite(r8) && b8 < 0x7F800000u)) b8 = 0x7F800000u;  // always pass
+                out8[i] = make_float2(__uint_as_float((__float_as_uint(uf) & ~0xFFu) | (b8 >> 24)),
+                                      __uint_as_float((__float_as_uint(vf) & ~0xFFu) | ((b8 >> 16) & 0xFFu)));
+            } else {
+                out8[i] = make_float2(uf, vf);
+            }
+        }
         rb = __float_as_uint(rr);
     }
     if (out8) {

@@ -196,3 +196,24 @@ def test_shadow_screen_annulus():
         assert m == 0
         print(n_sph, "passed / accepted", p / e)
         assert p <= 1.05 * e, (n_sph, p, e)
+
+
+@pytest.mark.parametrize("ld", LIGHTS)
+def test_packed_shadow_screen_never_rejects_an_accepted_sphere(spheres, ld):
+    """The same with each sphere's own rr' packed as bf16 into the low bytes of
+    its 8-byte {u, v} record (RT_SHD8_PER, oracle.c orc_shd8_screen_check):
+    no miss at the product's radius, some with it shrunk by 1%."""
+    L = _kernel_light(ld)
+    big_m = _bound(spheres)
+    rng = np.random.default_rng(13)
+    miss = passed = exact = tight = 0
+    for spread in (1e-7, 1e-6, 1e-5, 1e-3, 0.3):
+        o, idx = _shadow_pairs(spheres, L, 200_000, rng, spread, big_m)
+        m, p, e = oracle.shd8_screen_check(o, L, spheres, idx, big_m, SLACK_M, GROW)
+        miss += m
+        passed += p
+        exact += e
+        tight += oracle.shd8_screen_check(o, L, spheres, idx, big_m, SLACK_M, GROW, shrink=0.9)[0]
+    assert miss == 0, f"packed shadow screen rejected {miss} exactly-accepted pairs"
+    assert exact > 0 and passed >= exact
+    assert tight > 0
