@@ -1749,7 +1749,7 @@ __global__ void __launch_bounds__(kBlockThreads)
             if (RT_SHD8_PER) {
                 // this sphere's rr', grown by the stored centre's error (its
                 // 8 low mantissa bits a coordinate carry rr': <= 2^-15 |u|
-                // each), rounded up to bf16 (oracle.c orc_shd8_screen_check)
+                // each), rounded up to bf16 (its soundness test: tests/test_cam_screen.py)
                 const double ec = (1.0 / 16384.0) * (fabs(static_cast<double>(uf)) + fabs(static_cast<double>(vf)));
                 const double rg8 = rg + ec;
                 const float r8 = __double2float_ru(rg8 * rg8 * (1.0 + 4.0 * ur));
